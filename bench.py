@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark: captions/s (+ p50 encode+decode latency) for 16-frame ViT-B/16 -> GPT-2-small.
+
+BASELINE.json `metric`, quoted on configs[1]: batch=8 synthetic 16x3x224x224 videos, bf16,
+greedy decode on one MI355X.  One "step" = one pass of the hot path over one batch with the
+frames already resident in HBM: fused ViT encode + engine prefix + mapper (vcap_vit_encode),
+then the whole 24-token greedy decode with the reference generate()'s processors
+(repetition_penalty 1.1, no_repeat_ngram 3, min_new_tokens 8; text_decoder.py:131-144) as
+one replayed hipGraph (vcap_gpt2_generate).  For N>1 (torchrun, one rank per GPU) every rank
+encodes + decodes its own 8 videos (weak scaling, configs[2]) and the int32 token ids are
+gathered with one RCCL all_gather_into_tensor per step - the only collective.
+
+Rank 0 prints ONE JSON line.  `roofline` is priced on the dominant kernel (the ViT fc1 GEMM,
+`vcap_gemm_kernel<bf16,bf16,1>`), timed live with HIP events around each of its launches in
+the timed region (vcap_probe_*).  `cpu_baseline` times the CPU oracle (fp32 torch restatement
+of the reference path, oracle/vcap_oracle.py) on a bounded sample on the host cores (N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "video-caption-algorithm_amd"))
+sys.path.insert(0, str(ROOT))
+
+METRIC = "captions/sec + p50 encode+decode latency, 16-frame ViT-B/16 → GPT-2-small, 1/2/4/8 GPU"
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="videos per GPU")
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--max-new", type=int, default=24)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--decode", default="hf_greedy", choices=["hf_greedy", "raw_greedy"])
+    ap.add_argument("--vit", default="vit_base_patch16_224")
+    ap.add_argument("--gpt2", default="gpt2")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-baseline-s", type=float, default=20.0, help="CPU oracle time budget (0 disables)")
+    return ap.parse_args()
+
+
+def cpu_baseline(sd, va, ga, frames_np, budget_s: float, max_new: int):
+    """Time the CPU oracle (fp32) on ONE video at a time (the reference's single-video CPU path)."""
+    import torch
+    from oracle import vcap_oracle as O
+    threads = torch.get_num_threads()
+    video = torch.from_numpy(frames_np[:1])
+    times = []
+    t_start = time.perf_counter()
+    with torch.no_grad():
+        while True:
+            t0 = time.perf_counter()
+            ids = O.caption_ids(sd, va, ga, video, [ga.bos_token_id], max_new_tokens=max_new)
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_start > budget_s or len(times) >= 8:
+                break
+    p50 = statistics.median(times[1:] if len(times) > 1 else times)
+    return {"value": 1.0 / p50, "unit": "captions/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} single-video captions (1x16x3x224x224, fp32 torch CPU oracle, HF-greedy "
+                      f"max_new {max_new}); p50 of runs after the first = {p50 * 1e3:.0f} ms",
+            "p50_latency_ms": p50 * 1e3, "tokens_first": [int(t) for t in ids[0][:4]]}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from vcap import configs, prng, weights
+    from vcap import _native as N
+    from vcap.model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    va, ga = configs.vit_arch(args.vit), configs.gpt2_arch(args.gpt2)
+    sd = weights.synthetic_state_dict(1, va, ga)
+    B, T = args.batch, args.frames
+    frames_np = prng.imagenet_frames(1000 + rank, (B, T, 3, va.image, va.image))   # distinct videos per rank
+    video = torch.from_numpy(frames_np).to(dev)
+
+    enc = HipViTEncoder(sd, va, args.precision, dev)
+    pre = HipPrefix(sd, ga.n_embd, device=dev)
+    dec = HipGPT2Decoder(sd, ga, args.precision, dev)
+    if args.decode == "hf_greedy":
+        cfg = GenConfig(args.max_new, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, not args.no_graph)
+    else:
+        cfg = GenConfig.raw_greedy(args.max_new, ga.eos_token_id, not args.no_graph)
+    ids = torch.empty(B, args.max_new, dtype=torch.int32, device=dev)
+    gathered = torch.empty(world * B, args.max_new, dtype=torch.int32, device=dev) if world > 1 else None
+    stream = torch.cuda.Stream(dev)  # non-default stream: hipGraph replay + the probes' events live here
+
+    def step(ev=None):
+        e, prefix = enc.encode(video, pre)
+        if ev is not None:
+            ev.record()
+        dec.generate_ids(prefix, [ga.bos_token_id], cfg, out=ids)
+        if gathered is not None:
+            dist.all_gather_into_tensor(gathered, ids)
+
+    with torch.cuda.stream(stream):
+        for _ in range(max(args.warmup, 1)):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        lib = N.lib()
+        fc1_launches = va.depth * args.steps
+        N.check(lib.vcap_probe_enable(b"vit.fc1", fc1_launches), "probe")
+        N.check(lib.vcap_probe_enable(b"vit.attention", fc1_launches), "probe")
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        mids = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            starts[k].record()
+            step(mids[k])
+            ends[k].record()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    lat = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    vit_ms = [s.elapsed_time(m) for s, m in zip(starts, mids)]
+    dec_ms = [m.elapsed_time(e) for m, e in zip(mids, ends)]
+    fc1_total, fc1_n = N.C.c_float(), N.C.c_int()
+    N.check(lib.vcap_probe_read(b"vit.fc1", N.C.byref(fc1_total), N.C.byref(fc1_n)), "probe read")
+    at_total, at_n = N.C.c_float(), N.C.c_int()
+    N.check(lib.vcap_probe_read(b"vit.attention", N.C.byref(at_total), N.C.byref(at_n)), "probe read")
+
+    if rank == 0:
+        M = B * T * va.tokens
+        fc1_flops = 2.0 * M * va.mlp * va.dim
+        fc1_avg_s = fc1_total.value / max(fc1_n.value, 1) / 1e3
+        peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+        achieved = fc1_flops / fc1_avg_s / 1e12
+        attn_flops = 4.0 * B * T * va.heads * va.tokens * va.tokens * 64
+        attn_avg_s = at_total.value / max(at_n.value, 1) / 1e3
+        total = world * B * args.steps
+        value = total / elapsed
+        p50 = statistics.median(lat)
+        out = {
+            "metric": METRIC, "value": value, "unit": "captions/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.precision == "bf16" else "f32",
+            "data": "synthetic (seeded U[0,1) frames, ImageNet-normalised; seeded random-init weights)",
+            "config": {"workload": f"batch={B} synthetic {T}x3x224x224 videos per GPU, {args.vit} + {args.gpt2}, "
+                                   f"{args.decode} decode max_new {args.max_new} (BASELINE configs[1]"
+                                   f"{'/[2]' if world > 1 else ''})",
+                       "vit": args.vit, "gpt2": args.gpt2, "batch_per_gpu": B, "global_batch": world * B,
+                       "frames": T, "max_new_tokens": args.max_new, "decode": args.decode,
+                       "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}"},
+            "p50_latency_ms": p50, "captions_per_s_p50": world * B / (p50 / 1e3),
+            "stage_ms_p50": {"vit_encode_prefix": statistics.median(vit_ms), "gpt2_decode": statistics.median(dec_ms)},
+            "roofline": {"bound": "mfma", "kernel": "vit.fc1 vcap_gemm_kernel<bf16,bf16,1>",
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                         "traffic": None, "flops_per_launch": fc1_flops, "avg_launch_ms": fc1_avg_s * 1e3,
+                         "launches": fc1_n.value},
+            "attention": {"kernel": "vit.attention", "avg_launch_ms": attn_avg_s * 1e3,
+                          "achieved_tflops": attn_flops / attn_avg_s / 1e12,
+                          "frac_of_peak": attn_flops / attn_avg_s / 1e12 / peak},
+            "vit_flops_per_step": B * T * va.flops_per_frame(),
+        }
+        if world == 1 and args.cpu_baseline_s > 0:
+            out["cpu_baseline"] = cpu_baseline(sd, va, ga, frames_np, args.cpu_baseline_s, args.max_new)
+            out["cpu_baseline"].pop("tokens_first", None)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

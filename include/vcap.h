@@ -1,0 +1,142 @@
+/*
+ * vcap.h - C ABI of the MI355X-native video-caption hot path (libvcap_hip.so).
+ *
+ * Plain pointers and sizes only: device pointers are HIP device addresses, `stream` is a
+ * hipStream_t passed as void*.  Every entry point returns 0 on success or a negative code
+ * (-hipError_t, or VCAP_E_* for argument errors) and sets a thread-local message readable
+ * with vcap_last_error().  Nothing allocates device memory behind the caller's back: the
+ * caller owns the workspace (size from the *_workspace_bytes queries); nothing synchronises
+ * the stream.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo):
+ *   vcap_linear_bias        core/operators/cupy_linear_mapper.py:14-70 (linear_bias_f32/_f16 CUDA-C)
+ *                           and CuPyLinearCompat.forward :137-184 (nn.Linear drop-in)
+ *   vcap_vit_pool_temporal  core/operators/cupy_vit_pool.py:23-104 (vit_pool_{cls,gap}_{f32,f16}),
+ *                           vit_fused_pool_temporal :127-186
+ *   vcap_prefix_project     core/operators/normalization.py:6-13 apply_prefix_norm + the decoder
+ *                           mapper (src/models/text_decoder.py:249), i.e. core/engine.py:44-50 -> :60-74
+ *   vcap_gemm / vcap_layernorm / vcap_vit_attention
+ *                           the timm ViT block arithmetic the reference drives through
+ *                           src/models/video_encoder.py:112-174 (fused SDPA, tanh-GELU MLP,
+ *                           in-place residual) - op-level entry points for the plugin registry
+ *                           (core/operators/trt_plugin_hooks.py:7-34)
+ *   vcap_vit_encode         ViTFrameEncoder.forward (src/models/video_encoder.py:288-326) fused with
+ *                           the engine prefix (core/engine.py:43-50) and the mapper
+ *   vcap_gpt2_generate      GPT2TextDecoder.generate (src/models/text_decoder.py:105-146) ->
+ *                           GPT2LMHeadModel.generate greedy with RepetitionPenalty / NoRepeatNGram /
+ *                           MinNewTokens, and the raw greedy loop of
+ *                           core/scripts/benchmark_baseline.py:160-240 (processors disabled)
+ */
+#ifndef VCAP_H_
+#define VCAP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VCAP_ABI_VERSION 1
+
+enum { VCAP_DT_F32 = 0, VCAP_DT_BF16 = 1 };
+enum { VCAP_E_ARG = -1000, VCAP_E_WORKSPACE = -1001, VCAP_E_UNSUPPORTED = -1002 };
+
+typedef struct vcap_vit_layer {
+  const float* ln1_g; const float* ln1_b;
+  const void* qkv_w; const float* qkv_b;     /* [3D, D] */
+  const void* proj_w; const float* proj_b;   /* [D, D]  */
+  const float* ln2_g; const float* ln2_b;
+  const void* fc1_w; const float* fc1_b;     /* [4D, D] */
+  const void* fc2_w; const float* fc2_b;     /* [D, 4D] */
+} vcap_vit_layer;
+
+typedef struct vcap_vit_desc {
+  int dtype;                 /* operand dtype of the block GEMMs (VCAP_DT_*) */
+  int dim, depth, heads, patch, image, mlp, video_dim;
+  int kpad;                  /* patch K (3*p*p) padded to the GEMM K step */
+  float ln_eps;              /* 1e-6 (timm) */
+  const void* patch_w;       /* [dim, kpad] */
+  const float* patch_b;      /* [dim] */
+  const float* cls;          /* [dim] */
+  const float* pos;          /* [tokens, dim] */
+  const float* norm_g; const float* norm_b;
+  const float* proj_w;       /* encoder.proj [video_dim, dim] f32 */
+  const float* proj_b;
+  const vcap_vit_layer* layers;  /* host array of `depth` entries */
+} vcap_vit_desc;
+
+typedef struct vcap_prefix_desc {
+  float ln_scale;            /* <=0 disables the layer_norm*ln_scale step (core/engine.py:47) */
+  float in_weight;           /* <=0 disables the *in_weight step (core/engine.py:49) */
+  int prefix_len, n_embd;
+  const float* mapper_w;     /* [prefix_len*n_embd, video_dim] f32 */
+  const float* mapper_b;
+} vcap_prefix_desc;
+
+typedef struct vcap_gpt2_layer {
+  const float* ln1_g; const float* ln1_b;
+  const void* attn_w; const float* attn_b;   /* [3E, E] (Conv1D transposed) */
+  const void* aproj_w; const float* aproj_b; /* [E, E] */
+  const float* ln2_g; const float* ln2_b;
+  const void* fc_w; const float* fc_b;       /* [4E, E] */
+  const void* mproj_w; const float* mproj_b; /* [E, 4E] */
+} vcap_gpt2_layer;
+
+typedef struct vcap_gpt2_desc {
+  int dtype;
+  int n_embd, n_layer, n_head, vocab, n_positions, prefix_len;
+  float ln_eps;              /* 1e-5 */
+  const void* wte;           /* [vocab, E] (also the tied lm_head) */
+  const float* wpe;          /* [n_positions, E] f32 */
+  const float* lnf_g; const float* lnf_b;
+  const vcap_gpt2_layer* layers; /* host array of n_layer entries */
+} vcap_gpt2_desc;
+
+typedef struct vcap_gen_params {
+  int max_new_tokens;
+  int min_new_tokens;        /* 0 for raw greedy */
+  int no_repeat_ngram_size;  /* 0 disables */
+  float repetition_penalty;  /* 1.0 disables */
+  int eos_token_id, pad_token_id;
+  int use_graph;             /* capture the whole decode into a hipGraph and replay it */
+} vcap_gen_params;
+
+const char* vcap_last_error(void);
+int vcap_abi_version(void);
+
+/* ---- op-level entry points ---- */
+int vcap_linear_bias(int dtype, const void* x, const void* w, const float* b, void* y, int rows, int in_features,
+                     int out_features, void* stream);
+int vcap_gemm(int in_dtype, int out_dtype, const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
+              int64_t ldc, int M, int N, int K, const float* bias, int act, const float* res, int64_t ldr,
+              int res_mode, int G, int Gs, int goff, int roff, void* stream);
+int vcap_layernorm(int out_dtype, const float* x, int64_t ldx, void* y, int64_t ldy, const float* gamma,
+                   const float* beta, int rows, int dim, float eps, void* stream);
+int vcap_vit_attention(int dtype, const void* qkv, void* out, int frames, int tokens, int heads, void* stream);
+int vcap_vit_pool_temporal(int dtype, const void* feat, void* out, int bsz, int timesteps, int tokens, int channels,
+                           int pool_gap, void* stream);
+int vcap_prefix_project(const float* emb, int B, int video_dim, const vcap_prefix_desc* pd, float* prefix_out,
+                        void* stream);
+
+/* ---- fused paths ---- */
+size_t vcap_vit_workspace_bytes(const vcap_vit_desc* d, int B, int T);
+int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const float* frames, int B, int T,
+                    float* enc_out, float* prefix_out, void* workspace, size_t ws_bytes, void* stream);
+
+size_t vcap_gpt2_workspace_bytes(const vcap_gpt2_desc* d, int B, int S0, int max_new_tokens);
+int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* prompt_ids,
+                       int prompt_len, int B, int* out_ids, float* logits_out, void* workspace, size_t ws_bytes,
+                       void* stream);
+void vcap_graph_cache_clear(void);
+
+/* ---- live kernel timing for the benchmark's roofline (sites: "vit.qkv", "vit.attention",
+ *      "vit.proj", "vit.fc1", "vit.fc2"): events are recorded around each launch of the site on
+ *      the caller's stream, without synchronising; vcap_probe_read waits for them. ---- */
+int vcap_probe_enable(const char* site, int max_launches);
+int vcap_probe_read(const char* site, float* total_ms, int* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VCAP_H_ */

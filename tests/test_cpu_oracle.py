@@ -1,0 +1,127 @@
+"""CPU suite: the oracle (oracle/vcap_oracle.py) against the reference's recorded outputs,
+the portable PRNG, host-side decode bookkeeping, and the C ABI surface of libvcap_hip.so
+(load + every declared symbol; no compute calls without a GPU)."""
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import case, golden, pad_rows
+from oracle import vcap_oracle as O
+from vcap import _native as N
+from vcap import prng, weights, configs
+from vcap.model import raw_greedy_tokens, trim_generated
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _prefix_inputs(meta, sd, va, ga, frames):
+    video = torch.from_numpy(frames)
+    with torch.no_grad():
+        enc = O.encoder(sd, va, video)
+        pre = O.mapper(sd, O.prefix_norm(enc, meta["ln_scale"], meta["in_weight"]), ga.n_embd, 4)
+        x = O.build_inputs(sd, ga, pre, meta["prompt_ids"])
+    return enc, x
+
+
+@pytest.mark.parametrize("name", ["tiny", "tiny_prompt"])
+def test_oracle_matches_reference_tiny(name):
+    meta, g, va, ga, sd, frames = case(name)
+    assert weights_digest_ok(sd, meta)
+    enc, x = _prefix_inputs(meta, sd, va, ga, frames)
+    np.testing.assert_allclose(enc.numpy(), g["encoder_out"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(x.numpy(), g["inputs_embeds"], rtol=1e-5, atol=1e-6)
+    with torch.no_grad():
+        ids, lg = O.generate_greedy(sd, ga, x, return_logits=True)
+        raw = O.generate_raw_greedy(sd, ga, x)
+    assert np.array_equal(ids.numpy(), g["hf_greedy_ids"])
+    assert np.abs(torch.stack(lg[:3], 1).numpy() - g["hf_greedy_logits"]).max() < 1e-4
+    assert np.array_equal(pad_rows(raw, 24), g["raw_greedy_ids"])
+
+
+@pytest.mark.slow
+def test_oracle_matches_reference_b16_b2():
+    meta, g, va, ga, sd, frames = case("b16_b2")
+    enc, x = _prefix_inputs(meta, sd, va, ga, frames)
+    np.testing.assert_allclose(enc.numpy(), g["encoder_out"], rtol=1e-4, atol=1e-5)
+    with torch.no_grad():
+        ids, lg = O.generate_greedy(sd, ga, x, return_logits=True)
+    assert np.array_equal(ids.numpy(), g["hf_greedy_ids"])
+    for s in range(3):
+        got = np.take_along_axis(lg[s].numpy(), g[f"hf_greedy_logits_s{s}_top_i"].astype(np.int64), 1)
+        assert np.abs(got - g[f"hf_greedy_logits_s{s}_top_v"]).max() < 1e-4
+
+
+def weights_digest_ok(sd, meta):
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(sd[k], dtype=np.float32).tobytes())
+    return h.hexdigest() == meta["weights_sha256"]
+
+
+def test_prng_is_deterministic_and_shaped():
+    a = prng.normal(1, "x", (3, 5), 0.02)
+    b = prng.normal(1, "x", (3, 5), 0.02)
+    c = prng.normal(2, "x", (3, 5), 0.02)
+    assert a.dtype == np.float32 and a.shape == (3, 5)
+    assert np.array_equal(a, b) and not np.array_equal(a, c)
+    u = prng.uniform(0, "u", (100000,))
+    assert 0.0 <= u.min() and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.01
+    z = prng.normal(0, "z", (200000,))
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
+
+
+def test_ngram_ban_rule():
+    # NoRepeatNGramLogitsProcessor semantics (transformers logits_process.py)
+    assert O.banned_ngram_tokens([5, 6, 7, 5, 6], 3) == [7]
+    assert O.banned_ngram_tokens([5, 6], 3) == []
+    assert O.banned_ngram_tokens([1, 1, 1], 3) == [1]
+    assert O.banned_ngram_tokens([4, 4, 4, 4], 2) == [4, 4, 4]
+
+
+def test_trim_generated_matches_hf_stopping():
+    eos = 9
+    ids = torch.tensor([[1, 9, 9, 9], [2, 3, 9, 9]], dtype=torch.int32)
+    assert trim_generated(ids, eos) == [[1, 9, 9], [2, 3, 9]]
+    assert raw_greedy_tokens(ids, eos) == [[1, 9], [2, 3, 9]]
+    ids = torch.tensor([[1, 2, 3]], dtype=torch.int32)
+    assert trim_generated(ids, eos) == [[1, 2, 3]]
+
+
+def test_library_exports_every_header_symbol():
+    header = (ROOT / "include" / "vcap.h").read_text()
+    declared = set(re.findall(r"\b(vcap_[a-z0-9_]+)\s*\(", header))
+    assert declared == set(N.SIGNATURES), declared ^ set(N.SIGNATURES)
+    lib = N.lib()
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.vcap_abi_version() == N.ABI_VERSION
+
+
+def test_workspace_queries_without_gpu():
+    import ctypes as C
+    va, ga = configs.vit_arch("vit_base_patch16_224"), configs.gpt2_arch("gpt2")
+    layers = (N.VitLayer * va.depth)()
+    d = N.VitDesc(dtype=N.DT_BF16, dim=va.dim, depth=va.depth, heads=va.heads, patch=va.patch, image=va.image,
+                  mlp=va.mlp, video_dim=256, kpad=768, ln_eps=1e-6, layers=layers)
+    ws = N.lib().vcap_vit_workspace_bytes(C.byref(d), 8, 16)
+    M = 8 * 16 * 197
+    assert ws >= M * 768 * 4 + M * 3072 * 2
+    gl = (N.GPT2Layer * ga.n_layer)()
+    gd = N.GPT2Desc(dtype=N.DT_BF16, n_embd=768, n_layer=12, n_head=12, vocab=50257, n_positions=1024, prefix_len=4,
+                    ln_eps=1e-5, layers=gl)
+    assert N.lib().vcap_gpt2_workspace_bytes(C.byref(gd), 8, 5, 24) > 0
+    bad = N.VitDesc(dtype=N.DT_BF16, dim=100, depth=1, heads=1, patch=16, image=224, mlp=400, video_dim=256,
+                    kpad=768, ln_eps=1e-6, layers=layers)
+    assert N.lib().vcap_vit_workspace_bytes(C.byref(bad), 1, 1) == 0
+
+
+def test_golden_fixtures_are_self_consistent():
+    for name in ("tiny", "tiny_prompt", "b16_b2", "b16_b8"):
+        meta, g = golden(name)
+        assert g["hf_greedy_ids"].shape[0] == meta["B"]
+        assert meta["vit_vs_hf_vitmodel_maxabs"] < 1e-4  # restated timm ViT == transformers.ViTModel

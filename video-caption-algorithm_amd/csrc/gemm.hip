@@ -1,0 +1,185 @@
+// Tiled MFMA GEMM for the ViT hot loop (patch-embed, QKV, attn-proj, fc1, fc2) and the
+// prefix mapper:  C[M,N] = epilogue( A[M,K] . W[N,K]^T ).
+//
+// Replaces the reference's Linear layers inside timm Block/Attention/Mlp
+// (src/models/video_encoder.py:162-172 patched forward; GELU forced to tanh at :123-134)
+// and the CuPy `linear_bias_f32/_f16` kernels (core/operators/cupy_linear_mapper.py:14-70):
+// W keeps torch Linear's [out, in] row-major layout, so both operands are K-contiguous.
+//
+// Tile 128x128, 256 threads = 4 waves in 2x2, each wave 64x64 = 4x4 MFMA 16x16 tiles.
+// K step = 128 bytes per row (64 bf16 or 32 f32).  Operands stream global->LDS with
+// global_load_lds_dwordx4 (1 KiB per wave instruction, lane-linear LDS image); the
+// st_8x16B XOR swizzle (chunk ^ (row & 7)) is applied on the global SOURCE address and on
+// the ds_read address, making the ds_read_b128 fragment reads conflict-free.
+// bf16 uses mfma_f32_16x16x32_bf16; the fp32 parity mode uses mfma_f32_16x16x4f32 with the
+// SAME byte layout (one 16-byte chunk = 4 f32 = one group of four 16x16x4 MFMAs).
+#include "vcap_common.h"
+#include "vcap_kernels.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, ROWB = 128;  // ROWB: bytes of K per tile row
+constexpr int TILE_BYTES = BM * ROWB;          // 16 KiB per operand per stage
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+
+VCAP_DEV void glds16(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <typename T>
+VCAP_DEV void stage_tile(const T* __restrict__ P, long ld, int row0, int rows, int k0, char* lds_tile,
+                         int wave, int lane) {
+  constexpr int E = Frag<T>::kElems;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rb = wave * 4 + i;              // 8-row block written by this wave instruction
+    const int r = rb * 8 + (lane >> 3);
+    const int s = lane & 7;                   // LDS slot within the 128-byte row
+    const int c = s ^ (r & 7);                // global chunk stored in that slot
+    int gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    const T* src = P + (long)gr * ld + k0 + c * E;
+    glds16(src, lds_tile + rb * 1024);
+  }
+}
+
+VCAP_DEV u32x4 lds_frag(const char* tile, int row, int chunk) {
+  return *reinterpret_cast<const u32x4*>(tile + row * ROWB + ((chunk ^ (row & 7)) << 4));
+}
+
+}  // namespace
+
+// EPI (compile time, so each ViT GEMM role is its own kernel symbol in a profile):
+//   0 bias (QKV)   1 bias+gelu_tanh (fc1)   2 bias+residual in place (attn-proj, fc2)
+//   3 general: runtime act / residual mode / row remap (patch-embed, vcap_gemm ABI)
+template <typename TIn, typename TOut, int EPI>
+__global__ __launch_bounds__(256) void vcap_gemm_kernel(const TIn* __restrict__ A, long lda,
+                                                        const TIn* __restrict__ W, long ldw,
+                                                        TOut* C, long ldc, int M, int N, int K, GemmEpi epi) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  constexpr int E = Frag<TIn>::kElems;
+  constexpr int BK = ROWB / sizeof(TIn);
+
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD; give each XCD a contiguous run
+  // of tile ids so its L2 sees the same A row-panel across consecutive N tiles.
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
+  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  stage_tile(A, lda, m0, M, 0, smem, wave, lane);
+  stage_tile(W, ldw, n0, N, 0, smem + TILE_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE_BYTES;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
+      stage_tile(A, lda, m0, M, (kt + 1) * BK, nxt, wave, lane);
+      stage_tile(W, ldw, n0, N, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+    }
+    const char* ta = cur;
+    const char* tb = cur + TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u32x4 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = lds_frag(ta, wm * 64 + i * 16 + fr, s * 4 + fg);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = lds_frag(tb, wn * 64 + j * 16 + fr, s * 4 + fg);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_frag(af[i], bfr[j], acc[i][j], (TIn*)nullptr);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  (void)E;
+
+  // epilogue: lane holds rows fg*4 + r, column fr of each 16x16 tile
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + j * 16 + fr;
+    if (n >= N) continue;
+    const float bias = epi.bias ? epi.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + i * 16 + fg * 4 + r;
+        if (m >= M) continue;
+        float v = acc[i][j][r] + bias;
+        long orow = m;
+        if constexpr (EPI == 1) {
+          v = gelu_tanh(v);
+        } else if constexpr (EPI == 2) {
+          v += epi.res[orow * epi.ldr + n];
+        } else if constexpr (EPI == 3) {
+          if (epi.act == 1) v = gelu_tanh(v);
+          orow = epi.G ? (long)(m / epi.G) * epi.Gs + epi.goff + (m % epi.G) : (long)m;
+          if (epi.res_mode == 1) v += epi.res[orow * epi.ldr + n];
+          else if (epi.res_mode == 2) v += epi.res[(long)((m % epi.G) + epi.roff) * epi.ldr + n];
+        }
+        C[orow * ldc + n] = Num<TOut>::from_f(v);
+      }
+    }
+  }
+}
+
+template <typename TIn, typename TOut, int EPI>
+static hipError_t launch_gemm_epi(const void* A, long lda, const void* W, long ldw, void* C, long ldc, int M, int N,
+                                  int K, const GemmEpi& epi, hipStream_t s) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((vcap_gemm_kernel<TIn, TOut, EPI>), dim3(tiles), dim3(256), 0, s, (const TIn*)A, lda,
+                     (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, epi);
+  return hipGetLastError();
+}
+
+template <typename TIn, typename TOut>
+static hipError_t launch_gemm(const void* A, long lda, const void* W, long ldw, void* C, long ldc, int M, int N,
+                              int K, const GemmEpi& epi, hipStream_t s) {
+  const bool plain_rows = epi.G == 0;
+  if (plain_rows && epi.res_mode == 0 && epi.act == 0)
+    return launch_gemm_epi<TIn, TOut, 0>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if constexpr (sizeof(TOut) == sizeof(TIn)) {
+    if (plain_rows && epi.res_mode == 0 && epi.act == 1)
+      return launch_gemm_epi<TIn, TOut, 1>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  }
+  if constexpr (sizeof(TOut) == 4) {
+    if (plain_rows && epi.res_mode == 1 && epi.act == 0 && epi.res == (const float*)C && epi.ldr == ldc)
+      return launch_gemm_epi<TIn, TOut, 2>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  }
+  return launch_gemm_epi<TIn, TOut, 3>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+}
+
+// in_dt: operand dtype; out_dt: C dtype (the residual stream is f32)
+hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
+                              long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s) {
+  if (in_dt == VCAP_DT_BF16 && out_dt == VCAP_DT_BF16)
+    return launch_gemm<bf16_t, bf16_t>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if (in_dt == VCAP_DT_BF16 && out_dt == VCAP_DT_F32)
+    return launch_gemm<bf16_t, float>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if (in_dt == VCAP_DT_F32 && out_dt == VCAP_DT_F32)
+    return launch_gemm<float, float>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  return hipErrorInvalidValue;
+}
+
+int vcap_gemm_k_align(int in_dt) { return in_dt == VCAP_DT_BF16 ? 64 : 32; }

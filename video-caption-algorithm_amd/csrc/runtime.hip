@@ -1,0 +1,527 @@
+// Host runtime behind the C ABI (include/vcap.h): argument checking, workspace carving, the
+// ViT forward schedule, the GPT-2 decode schedule and its hipGraph cache.
+//
+// The reference drives these steps from Python (timm forward_features, HF generate); here the
+// whole schedule is native so one ABI call issues the full encode or the full decode, and the
+// decode (~60 launches per token) can be captured once into a hipGraph and replayed.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/vcap.h"
+#include "vcap_common.h"
+#include "vcap_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  if (e == hipSuccess) return 0;
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return -(int)e;
+}
+
+#define VCAP_TRY(expr, where)                    \
+  do {                                           \
+    hipError_t _e = (expr);                      \
+    if (_e != hipSuccess) return hip_fail(_e, where); \
+  } while (0)
+
+size_t esize(int dt) { return dt == VCAP_DT_BF16 ? 2 : 4; }
+size_t al(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  explicit Carver(void* b) : base((char*)b) {}
+  void* take(size_t bytes) {
+    void* p = base ? base + off : nullptr;
+    off += al(bytes);
+    return p;
+  }
+};
+
+bool attn_lds_configured = false;
+
+// ----------------------------------------------------------------------------------- kernel probes
+// Live per-site timing for bench.py's roofline: HIP events recorded around every launch of a
+// probed site on the caller's stream (no synchronisation; read back after the timed region).
+struct Probe {
+  std::vector<hipEvent_t> start, stop;
+  int used = 0;
+  bool on = false;
+};
+std::mutex g_probe_mu;
+std::unordered_map<std::string, Probe> g_probes;
+
+Probe* probe_for(const char* site) {
+  std::lock_guard<std::mutex> lk(g_probe_mu);
+  auto it = g_probes.find(site);
+  if (it == g_probes.end() || !it->second.on || it->second.used >= (int)it->second.start.size()) return nullptr;
+  return &it->second;
+}
+
+struct ProbeScope {
+  Probe* p;
+  hipStream_t s;
+  int idx;
+  ProbeScope(const char* site, hipStream_t st) : p(probe_for(site)), s(st), idx(-1) {
+    if (p) {
+      idx = p->used++;
+      (void)hipEventRecord(p->start[idx], s);
+    }
+  }
+  ~ProbeScope() {
+    if (p) (void)hipEventRecord(p->stop[idx], s);
+  }
+};
+
+
+// ----------------------------------------------------------------------------------- ViT
+struct VitBufs {
+  float* x;
+  void* xn;
+  void* qkv;
+  void* attn;
+  void* act;
+};
+
+VitBufs carve_vit(Carver& c, const vcap_vit_desc* d, int B, int T) {
+  const int tokens = (d->image / d->patch) * (d->image / d->patch) + 1;
+  const size_t M = (size_t)B * T * tokens;
+  const size_t es = esize(d->dtype);
+  const size_t npatch = (size_t)B * T * (tokens - 1);
+  VitBufs v;
+  v.x = (float*)c.take(M * d->dim * 4);
+  v.xn = c.take(M * d->dim * es);
+  v.qkv = c.take(M * 3 * d->dim * es);
+  v.attn = c.take(M * d->dim * es);
+  size_t act = M * d->mlp * es;
+  const size_t patches = npatch * d->kpad * es;
+  v.act = c.take(act > patches ? act : patches);
+  return v;
+}
+
+int check_vit(const vcap_vit_desc* d) {
+  if (!d || !d->layers) return fail(VCAP_E_ARG, "vit desc is null");
+  if (d->dtype != VCAP_DT_F32 && d->dtype != VCAP_DT_BF16) return fail(VCAP_E_ARG, "vit dtype");
+  if (d->heads * 64 != d->dim) return fail(VCAP_E_UNSUPPORTED, "vit head_dim must be 64");
+  const int ka = vcap_gemm_k_align(d->dtype);
+  if (d->dim % ka || d->mlp % ka || d->kpad % ka || d->kpad < 3 * d->patch * d->patch)
+    return fail(VCAP_E_UNSUPPORTED, "vit dims must be multiples of the GEMM K step");
+  if (d->image % d->patch) return fail(VCAP_E_ARG, "image not divisible by patch");
+  const int tokens = (d->image / d->patch) * (d->image / d->patch) + 1;
+  if (tokens > 288) return fail(VCAP_E_UNSUPPORTED, "more than 288 tokens");
+  return 0;
+}
+
+// ----------------------------------------------------------------------------------- GPT-2
+struct DecBufs {
+  float* h;
+  void* q;
+  void* attn;
+  void* act;
+  void* xn;
+  void* kc;
+  void* vc;
+  int* pt;
+  float* pval;
+  int* pidx;
+  int* hist;
+  int* banned;
+  int* nbanned;
+  int* finished;
+};
+
+int max_logit_blocks(int V, int B) { return vcap_logit_blocks(V, B); }
+
+DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new, int* maxp_out, size_t* page_elems) {
+  const int E = d->n_embd;
+  const size_t es = esize(d->dtype);
+  const size_t Mmax = (size_t)B * S0 > (size_t)B ? (size_t)B * S0 : B;
+  const int maxp = (S0 + max_new + 15) / 16;
+  *maxp_out = maxp;
+  const size_t pages = (size_t)B * maxp;
+  const size_t per_layer = pages * d->n_head * 16 * 64;  // elements
+  *page_elems = per_layer;
+  DecBufs b;
+  b.h = (float*)c.take(Mmax * E * 4);
+  b.q = c.take(Mmax * E * es);
+  b.attn = c.take(Mmax * E * es);
+  b.act = c.take(Mmax * 4 * E * es);
+  b.xn = c.take((size_t)B * E * es);
+  b.kc = c.take(per_layer * d->n_layer * es);
+  b.vc = c.take(per_layer * d->n_layer * es);
+  b.pt = (int*)c.take(pages * 4);
+  const int nb = max_logit_blocks(d->vocab, B);
+  b.pval = (float*)c.take((size_t)B * nb * 4);
+  b.pidx = (int*)c.take((size_t)B * nb * 4);
+  b.hist = (int*)c.take((size_t)B * max_new * 4);
+  b.banned = (int*)c.take((size_t)B * max_new * 4);
+  b.nbanned = (int*)c.take((size_t)B * 4);
+  b.finished = (int*)c.take((size_t)B * 4);
+  return b;
+}
+
+int check_gpt2(const vcap_gpt2_desc* d) {
+  if (!d || !d->layers) return fail(VCAP_E_ARG, "gpt2 desc is null");
+  if (d->dtype != VCAP_DT_F32 && d->dtype != VCAP_DT_BF16) return fail(VCAP_E_ARG, "gpt2 dtype");
+  if (d->n_head * 64 != d->n_embd) return fail(VCAP_E_UNSUPPORTED, "gpt2 head_dim must be 64");
+  if (d->n_embd % 64) return fail(VCAP_E_UNSUPPORTED, "n_embd must be a multiple of 64");
+  return 0;
+}
+
+int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* ids, int nids,
+                 int B, int* out_ids, float* logits_out, const DecBufs& w, int maxp, size_t page_elems,
+                 hipStream_t s) {
+  const int E = d->n_embd, H = d->n_head, L = d->n_layer, V = d->vocab;
+  const int P = d->prefix_len, S0 = P + nids, max_new = gp->max_new_tokens;
+  const int dt = d->dtype;
+  const size_t es = esize(dt);
+  VCAP_TRY(vcap_decode_init_dispatch(w.pt, B, maxp, w.finished, w.nbanned, s), "decode_init");
+  VCAP_TRY(vcap_prefill_embed_dispatch(dt, prefix, P, ids, nids, d->wte, d->wpe, w.h, B, E, s), "prefill_embed");
+  for (int step = 0; step < max_new; ++step) {
+    const int S_new = step == 0 ? S0 : 1;
+    const int past = step == 0 ? 0 : S0 + step - 1;
+    const int M = B * S_new;
+    for (int l = 0; l < L; ++l) {
+      const vcap_gpt2_layer& ly = d->layers[l];
+      RowsGemmArgs a;
+      memset(&a, 0, sizeof(a));
+      a.M = M;
+      a.ln_eps = d->ln_eps;
+      // 1) ln_1 + c_attn -> q, paged K/V
+      a.x = w.h; a.ldx = E; a.ln_g = ly.ln1_g; a.ln_b = ly.ln1_b;
+      a.w = ly.attn_w; a.ldw = E; a.bias = ly.attn_b; a.N = 3 * E; a.K = E;
+      a.q_out = w.q;
+      a.kc = (char*)w.kc + (size_t)l * page_elems * es;
+      a.vc = (char*)w.vc + (size_t)l * page_elems * es;
+      a.page_table = w.pt; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past;
+      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
+      // 2) causal attention over the paged cache
+      VCAP_TRY(vcap_decode_attention_dispatch(dt, w.q, a.kc, a.vc, w.pt, maxp, w.attn, M, H, S_new, past, s),
+               "decode_attention");
+      // 3) attn c_proj + residual
+      RowsGemmArgs b;
+      memset(&b, 0, sizeof(b));
+      b.M = M; b.x = w.attn; b.ldx = E; b.w = ly.aproj_w; b.ldw = E; b.bias = ly.aproj_b; b.N = E; b.K = E;
+      b.out = w.h; b.ldo = E;
+      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, b, nullptr, s), "attn_c_proj");
+      // 4) ln_2 + c_fc + gelu_new
+      RowsGemmArgs c;
+      memset(&c, 0, sizeof(c));
+      c.M = M; c.x = w.h; c.ldx = E; c.ln_g = ly.ln2_g; c.ln_b = ly.ln2_b; c.ln_eps = d->ln_eps;
+      c.w = ly.fc_w; c.ldw = E; c.bias = ly.fc_b; c.N = 4 * E; c.K = E; c.out = w.act; c.ldo = 4 * E;
+      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_GELU, c, nullptr, s), "c_fc");
+      // 5) mlp c_proj + residual
+      RowsGemmArgs e;
+      memset(&e, 0, sizeof(e));
+      e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.ldw = 4 * E; e.bias = ly.mproj_b; e.N = E;
+      e.K = 4 * E; e.out = w.h; e.ldo = E;
+      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, e, nullptr, s), "mlp_c_proj");
+    }
+    // ln_f on each sequence's last row, then the tied lm_head with fused processors + argmax partials
+    VCAP_TRY(vcap_layernorm_dispatch(dt, w.h + (size_t)(S_new - 1) * E, (long)S_new * E, w.xn, E, d->lnf_g,
+                                     d->lnf_b, B, E, d->ln_eps, s),
+             "ln_f");
+    RowsGemmArgs g;
+    memset(&g, 0, sizeof(g));
+    g.M = B; g.x = w.xn; g.ldx = E; g.w = d->wte; g.ldw = E; g.bias = nullptr; g.N = V; g.K = E;
+    g.logits_raw = logits_out ? logits_out + (size_t)step * B * V : nullptr;
+    g.part_val = w.pval; g.part_idx = w.pidx;
+    g.nblk = max_logit_blocks(V, B);
+    g.hist = w.hist; g.hist_ld = max_new; g.gen_len = step; g.banned = w.banned; g.nbanned = w.nbanned;
+    g.rep_penalty = gp->repetition_penalty; g.min_new = gp->min_new_tokens; g.eos = gp->eos_token_id;
+    int nblk = 0;
+    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_LOGITS, g, &nblk, s), "lm_head");
+    VCAP_TRY(vcap_decode_finalize_dispatch(dt, w.pval, w.pidx, nblk, B, step, w.finished, w.hist, max_new, w.banned,
+                                           w.nbanned, gp->no_repeat_ngram_size, gp->eos_token_id, gp->pad_token_id,
+                                           out_ids, max_new, d->wte, d->wpe, w.h, E,
+                                           (S0 + step) < d->n_positions ? S0 + step : d->n_positions - 1, s),
+             "finalize");
+  }
+  return 0;
+}
+
+// ----------------------------------------------------------------------------------- graph cache
+struct GraphEntry {
+  hipGraphExec_t exec = nullptr;
+};
+std::mutex g_graph_mu;
+std::unordered_map<std::string, GraphEntry> g_graphs;
+std::unordered_map<int, hipStream_t> g_capture_streams;
+
+std::string graph_key(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* ids,
+                      int nids, int B, const int* out_ids, const float* logits, const void* ws) {
+  std::string k;
+  auto put = [&](const void* p, size_t n) { k.append((const char*)p, n); };
+  put(d, sizeof(*d));
+  for (int l = 0; l < d->n_layer; ++l) put(&d->layers[l], sizeof(vcap_gpt2_layer));
+  put(gp, sizeof(*gp));
+  put(&prefix, sizeof(prefix));
+  put(ids, sizeof(int) * (size_t)nids);
+  put(&nids, sizeof(nids));
+  put(&B, sizeof(B));
+  put(&out_ids, sizeof(out_ids));
+  put(&logits, sizeof(logits));
+  put(&ws, sizeof(ws));
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  put(&dev, sizeof(dev));
+  return k;
+}
+
+}  // namespace
+
+// =====================================================================================================
+extern "C" {
+
+const char* vcap_last_error(void) { return g_err.c_str(); }
+int vcap_abi_version(void) { return VCAP_ABI_VERSION; }
+
+int vcap_gemm(int in_dtype, int out_dtype, const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
+              int64_t ldc, int M, int N, int K, const float* bias, int act, const float* res, int64_t ldr,
+              int res_mode, int G, int Gs, int goff, int roff, void* stream) {
+  if (!A || !W || !C || M <= 0 || N <= 0 || K <= 0) return fail(VCAP_E_ARG, "vcap_gemm: bad arguments");
+  if (K % vcap_gemm_k_align(in_dtype)) return fail(VCAP_E_UNSUPPORTED, "vcap_gemm: K must be a multiple of the K step");
+  if (res_mode && !res) return fail(VCAP_E_ARG, "vcap_gemm: residual pointer missing");
+  if ((res_mode == 2 || G) && G <= 0) return fail(VCAP_E_ARG, "vcap_gemm: row group G must be > 0");
+  if (res_mode && out_dtype != VCAP_DT_F32) return fail(VCAP_E_UNSUPPORTED, "vcap_gemm: residual needs f32 output");
+  GemmEpi e{bias, res, (long)ldr, act, res_mode, G, Gs, goff, roff};
+  g_err.clear();
+  VCAP_TRY(vcap_gemm_dispatch(in_dtype, out_dtype, A, lda, W, ldw, C, ldc, M, N, K, e, (hipStream_t)stream),
+           "vcap_gemm");
+  return 0;
+}
+
+int vcap_linear_bias(int dtype, const void* x, const void* w, const float* b, void* y, int rows, int in_features,
+                     int out_features, void* stream) {
+  return vcap_gemm(dtype, dtype, x, in_features, w, in_features, y, out_features, rows, out_features, in_features, b,
+                   0, nullptr, 0, 0, 0, 0, 0, 0, stream);
+}
+
+int vcap_layernorm(int out_dtype, const float* x, int64_t ldx, void* y, int64_t ldy, const float* gamma,
+                   const float* beta, int rows, int dim, float eps, void* stream) {
+  if (!x || !y || rows < 0 || dim <= 0) return fail(VCAP_E_ARG, "vcap_layernorm: bad arguments");
+  if ((gamma == nullptr) != (beta == nullptr)) return fail(VCAP_E_ARG, "vcap_layernorm: gamma/beta mismatch");
+  VCAP_TRY(vcap_layernorm_dispatch(out_dtype, x, (long)ldx, y, (long)ldy, gamma, beta, rows, dim, eps,
+                                   (hipStream_t)stream),
+           "vcap_layernorm");
+  return 0;
+}
+
+static int ensure_attn_lds() {
+  if (attn_lds_configured) return 0;
+  attn_lds_configured = true;
+  return 0;
+}
+
+int vcap_vit_attention(int dtype, const void* qkv, void* out, int frames, int tokens, int heads, void* stream) {
+  if (!qkv || !out || frames <= 0 || tokens <= 0 || heads <= 0) return fail(VCAP_E_ARG, "vcap_vit_attention: bad arguments");
+  if (tokens > 288) return fail(VCAP_E_UNSUPPORTED, "vcap_vit_attention: tokens > 288");
+  ensure_attn_lds();
+  VCAP_TRY(vcap_vit_attention_dispatch(dtype, qkv, out, frames, tokens, heads, (hipStream_t)stream),
+           "vcap_vit_attention");
+  return 0;
+}
+
+int vcap_vit_pool_temporal(int dtype, const void* feat, void* out, int bsz, int timesteps, int tokens, int channels,
+                           int pool_gap, void* stream) {
+  if (!feat || !out || bsz <= 0 || timesteps <= 0 || tokens <= 0 || channels <= 0)
+    return fail(VCAP_E_ARG, "vcap_vit_pool_temporal: bad arguments");
+  if (pool_gap && tokens <= 1) return fail(VCAP_E_ARG, "vcap_vit_pool_temporal: gap needs tokens > 1");
+  VCAP_TRY(vcap_vit_pool_dispatch(dtype, feat, out, bsz, timesteps, tokens, channels, pool_gap, (hipStream_t)stream),
+           "vcap_vit_pool_temporal");
+  return 0;
+}
+
+int vcap_prefix_project(const float* emb, int B, int video_dim, const vcap_prefix_desc* pd, float* prefix_out,
+                        void* stream) {
+  if (!emb || !pd || !prefix_out || !pd->mapper_w || B <= 0) return fail(VCAP_E_ARG, "vcap_prefix_project: bad arguments");
+  if (video_dim > 1024) return fail(VCAP_E_UNSUPPORTED, "video_dim > 1024");
+  VCAP_TRY(vcap_vit_head_prefix_dispatch(nullptr, B, 1, 1, 1, nullptr, nullptr, 0.f, nullptr, nullptr, video_dim,
+                                         pd->ln_scale, pd->in_weight, pd->mapper_w, pd->mapper_b,
+                                         pd->prefix_len * pd->n_embd, nullptr, prefix_out, emb, (hipStream_t)stream),
+           "vcap_prefix_project");
+  return 0;
+}
+
+size_t vcap_vit_workspace_bytes(const vcap_vit_desc* d, int B, int T) {
+  if (check_vit(d)) return 0;
+  Carver c(nullptr);
+  carve_vit(c, d, B, T);
+  return c.off;
+}
+
+int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const float* frames, int B, int T,
+                    float* enc_out, float* prefix_out, void* workspace, size_t ws_bytes, void* stream) {
+  if (int rc = check_vit(d)) return rc;
+  if (!frames || !enc_out || B <= 0 || T <= 0) return fail(VCAP_E_ARG, "vcap_vit_encode: bad arguments");
+  if (prefix_out && (!pd || !pd->mapper_w)) return fail(VCAP_E_ARG, "vcap_vit_encode: prefix desc missing");
+  if (ws_bytes < vcap_vit_workspace_bytes(d, B, T)) return fail(VCAP_E_WORKSPACE, "vcap_vit_encode: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  Carver c(workspace);
+  VitBufs w = carve_vit(c, d, B, T);
+  const int dt = d->dtype, D = d->dim, g = d->image / d->patch, P = g * g, N = P + 1, BT = B * T;
+  const int M = BT * N;
+  // patch embedding: im2col + GEMM whose epilogue adds bias + pos[1+p] and scatters row bt*N+1+p
+  VCAP_TRY(vcap_patchify_dispatch(dt, frames, w.act, w.x, d->cls, d->pos, BT, d->image, d->patch, d->kpad, N, D, s),
+           "patchify");
+  GemmEpi pe{d->patch_b, d->pos, D, 0, 2, P, N, 1, 1};
+  VCAP_TRY(vcap_gemm_dispatch(dt, VCAP_DT_F32, w.act, d->kpad, d->patch_w, d->kpad, w.x, D, BT * P, D, d->kpad, pe, s),
+           "patch_gemm");
+  for (int l = 0; l < d->depth; ++l) {
+    const vcap_vit_layer& ly = d->layers[l];
+    VCAP_TRY(vcap_layernorm_dispatch(dt, w.x, D, w.xn, D, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s), "norm1");
+    GemmEpi e1{ly.qkv_b, nullptr, 0, 0, 0, 0, 0, 0, 0};
+    {
+      ProbeScope ps("vit.qkv", s);
+      VCAP_TRY(vcap_gemm_dispatch(dt, dt, w.xn, D, ly.qkv_w, D, w.qkv, 3 * D, M, 3 * D, D, e1, s), "qkv");
+    }
+    {
+      ProbeScope ps("vit.attention", s);
+      VCAP_TRY(vcap_vit_attention_dispatch(dt, w.qkv, w.attn, BT, N, d->heads, s), "attention");
+    }
+    GemmEpi e2{ly.proj_b, w.x, D, 0, 1, 0, 0, 0, 0};
+    {
+      ProbeScope ps("vit.proj", s);
+      VCAP_TRY(vcap_gemm_dispatch(dt, VCAP_DT_F32, w.attn, D, ly.proj_w, D, w.x, D, M, D, D, e2, s), "attn_proj");
+    }
+    VCAP_TRY(vcap_layernorm_dispatch(dt, w.x, D, w.xn, D, ly.ln2_g, ly.ln2_b, M, D, d->ln_eps, s), "norm2");
+    GemmEpi e3{ly.fc1_b, nullptr, 0, 1, 0, 0, 0, 0, 0};
+    {
+      ProbeScope ps("vit.fc1", s);
+      VCAP_TRY(vcap_gemm_dispatch(dt, dt, w.xn, D, ly.fc1_w, D, w.act, d->mlp, M, d->mlp, D, e3, s), "fc1");
+    }
+    GemmEpi e4{ly.fc2_b, w.x, D, 0, 1, 0, 0, 0, 0};
+    {
+      ProbeScope ps("vit.fc2", s);
+      VCAP_TRY(vcap_gemm_dispatch(dt, VCAP_DT_F32, w.act, d->mlp, ly.fc2_w, d->mlp, w.x, D, M, D, d->mlp, e4, s), "fc2");
+    }
+  }
+  const float ls = pd ? pd->ln_scale : 0.f, iw = pd ? pd->in_weight : 0.f;
+  const int MO = pd ? pd->prefix_len * pd->n_embd : 0;
+  VCAP_TRY(vcap_vit_head_prefix_dispatch(w.x, B, T, N, D, d->norm_g, d->norm_b, d->ln_eps, d->proj_w, d->proj_b,
+                                         d->video_dim, ls, iw, pd ? pd->mapper_w : nullptr,
+                                         pd ? pd->mapper_b : nullptr, MO, enc_out, prefix_out, nullptr, s),
+           "head_prefix");
+  return 0;
+}
+
+size_t vcap_gpt2_workspace_bytes(const vcap_gpt2_desc* d, int B, int S0, int max_new_tokens) {
+  if (check_gpt2(d)) return 0;
+  Carver c(nullptr);
+  int maxp;
+  size_t pe;
+  carve_dec(c, d, B, S0, max_new_tokens, &maxp, &pe);
+  return c.off;
+}
+
+int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* prompt_ids,
+                       int prompt_len, int B, int* out_ids, float* logits_out, void* workspace, size_t ws_bytes,
+                       void* stream) {
+  if (int rc = check_gpt2(d)) return rc;
+  if (!gp || !prefix || !out_ids || B <= 0 || prompt_len < 0 || prompt_len > 64 || (prompt_len && !prompt_ids))
+    return fail(VCAP_E_ARG, "vcap_gpt2_generate: bad arguments");
+  if (gp->max_new_tokens <= 0) return fail(VCAP_E_ARG, "max_new_tokens must be > 0");
+  const int S0 = d->prefix_len + prompt_len;
+  if (S0 <= 0 || B * S0 > 128) return fail(VCAP_E_UNSUPPORTED, "B*(prefix+prompt) must be <= 128 rows");
+  if (S0 + gp->max_new_tokens > d->n_positions || S0 + gp->max_new_tokens > 1024)
+    return fail(VCAP_E_UNSUPPORTED, "context exceeds n_positions");
+  for (int i = 0; i < prompt_len; ++i)
+    if (prompt_ids[i] < 0 || prompt_ids[i] >= d->vocab) return fail(VCAP_E_ARG, "prompt id out of range");
+  if (ws_bytes < vcap_gpt2_workspace_bytes(d, B, S0, gp->max_new_tokens))
+    return fail(VCAP_E_WORKSPACE, "vcap_gpt2_generate: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  Carver c(workspace);
+  int maxp;
+  size_t page_elems;
+  DecBufs w = carve_dec(c, d, B, S0, gp->max_new_tokens, &maxp, &page_elems);
+  if (!gp->use_graph)
+    return issue_decode(d, gp, prefix, prompt_ids, prompt_len, B, out_ids, logits_out, w, maxp, page_elems, s);
+
+  const std::string key = graph_key(d, gp, prefix, prompt_ids, prompt_len, B, out_ids, logits_out, workspace);
+  std::lock_guard<std::mutex> lk(g_graph_mu);
+  auto it = g_graphs.find(key);
+  if (it == g_graphs.end()) {
+    int dev = 0;
+    VCAP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    hipStream_t cs = g_capture_streams[dev];
+    if (!cs) {
+      VCAP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "hipStreamCreate");
+      g_capture_streams[dev] = cs;
+    }
+    VCAP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    int rc = issue_decode(d, gp, prefix, prompt_ids, prompt_len, B, out_ids, logits_out, w, maxp, page_elems, cs);
+    hipGraph_t graph = nullptr;
+    hipError_t ec = hipStreamEndCapture(cs, &graph);
+    if (rc) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    VCAP_TRY(ec, "hipStreamEndCapture");
+    GraphEntry ge;
+    hipError_t ei = hipGraphInstantiate(&ge.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    VCAP_TRY(ei, "hipGraphInstantiate");
+    it = g_graphs.emplace(key, ge).first;
+  }
+  VCAP_TRY(hipGraphLaunch(it->second.exec, s), "hipGraphLaunch");
+  return 0;
+}
+
+int vcap_probe_enable(const char* site, int max_launches) {
+  if (!site || max_launches <= 0) return fail(VCAP_E_ARG, "vcap_probe_enable: bad arguments");
+  std::lock_guard<std::mutex> lk(g_probe_mu);
+  Probe& p = g_probes[site];
+  while ((int)p.start.size() < max_launches) {
+    hipEvent_t a, b;
+    VCAP_TRY(hipEventCreate(&a), "hipEventCreate");
+    VCAP_TRY(hipEventCreate(&b), "hipEventCreate");
+    p.start.push_back(a);
+    p.stop.push_back(b);
+  }
+  p.used = 0;
+  p.on = true;
+  return 0;
+}
+
+int vcap_probe_read(const char* site, float* total_ms, int* launches) {
+  if (!site || !total_ms || !launches) return fail(VCAP_E_ARG, "vcap_probe_read: bad arguments");
+  std::lock_guard<std::mutex> lk(g_probe_mu);
+  auto it = g_probes.find(site);
+  *total_ms = 0.f;
+  *launches = 0;
+  if (it == g_probes.end()) return 0;
+  Probe& p = it->second;
+  for (int i = 0; i < p.used; ++i) {
+    VCAP_TRY(hipEventSynchronize(p.stop[i]), "hipEventSynchronize");
+    float ms = 0.f;
+    VCAP_TRY(hipEventElapsedTime(&ms, p.start[i], p.stop[i]), "hipEventElapsedTime");
+    *total_ms += ms;
+  }
+  *launches = p.used;
+  p.on = false;
+  p.used = 0;
+  return 0;
+}
+
+void vcap_graph_cache_clear(void) {
+  std::lock_guard<std::mutex> lk(g_graph_mu);
+  for (auto& kv : g_graphs)
+    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+  g_graphs.clear();
+}
+
+}  // extern "C"

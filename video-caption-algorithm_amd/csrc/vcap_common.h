@@ -1,0 +1,82 @@
+// Shared device helpers for the vcap HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VCAP_DEV __device__ __forceinline__
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA 16x16x32 bf16 A/B fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4;    // MFMA 16x16 accumulator / f32 fragment
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+
+VCAP_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+VCAP_DEV bf16_t f2bf(float f) {
+  // round-to-nearest-even; inputs here are finite activations/weights
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+VCAP_DEV uint32_t pack_bf2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+template <typename T> struct Num;
+template <> struct Num<float> {
+  static VCAP_DEV float to_f(float v) { return v; }
+  static VCAP_DEV float from_f(float v) { return v; }
+};
+template <> struct Num<bf16_t> {
+  static VCAP_DEV float to_f(bf16_t v) { return bf2f(v); }
+  static VCAP_DEV bf16_t from_f(float v) { return f2bf(v); }
+};
+
+// tanh-approximate GELU, the form both torch's GELU(approximate="tanh")
+// (ViT MLP, src/models/video_encoder.py:123-134) and HF gelu_new (GPT-2 MLP) compute.
+VCAP_DEV float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
+  const float k1 = 0.044715f;
+  float inner = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.0f + tanhf(inner));
+}
+
+VCAP_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+VCAP_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// MFMA wrappers. Both consume one 16-byte fragment per lane per call group:
+//  bf16: lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15], j=0..7 (one 16x16x32)
+//  f32 : lane l holds A[l&15][4(l>>4)+i], B[4(l>>4)+i][l&15], i=0..3 as FOUR 16x16x4
+//        calls (call i uses element i: k index 4g+i for lane group g; the k order is a
+//        permutation applied identically to A and B, so the sum is exact f32 FMA chain).
+VCAP_DEV f32x4 mfma_frag(const u32x4& a, const u32x4& b, f32x4 c, bf16_t*) {
+  bf16x8 av = __builtin_bit_cast(bf16x8, a);
+  bf16x8 bv = __builtin_bit_cast(bf16x8, b);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c, 0, 0, 0);
+}
+VCAP_DEV f32x4 mfma_frag(const u32x4& a, const u32x4& b, f32x4 c, float*) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
+  return c;
+}
+
+// elements of T per 16-byte fragment chunk
+template <typename T> struct Frag { static constexpr int kElems = 16 / sizeof(T); };
+
+#ifndef VCAP_H_
+enum { VCAP_DT_F32 = 0, VCAP_DT_BF16 = 1 };  // mirrors include/vcap.h
+#endif

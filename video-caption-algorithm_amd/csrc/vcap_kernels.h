@@ -1,0 +1,73 @@
+// Kernel-side interface shared by the .hip translation units and the host runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+
+struct GemmEpi {
+  const float* bias;  // [N] or nullptr
+  const float* res;   // residual source (f32) or nullptr
+  long ldr;           // residual row stride (elements)
+  int act;            // 0 none, 1 gelu_tanh
+  int res_mode;       // 0 none, 1 residual row == output row (may alias C), 2 row (m % G) + roff
+  int G, Gs, goff;    // output row remap: G ? (m/G)*Gs + goff + m%G : m
+  int roff;
+};
+
+enum { PRO_LN = 0, PRO_DIRECT = 1 };
+enum { EPI_QKV = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_LOGITS = 3, EPI_STORE = 4 };
+
+struct RowsGemmArgs {
+  const void* x;  // PRO_LN: f32 residual rows; PRO_DIRECT: T rows
+  long ldx;
+  const float* ln_g;
+  const float* ln_b;
+  float ln_eps;
+  const void* w;  // T [N, K]
+  long ldw;
+  const float* bias;
+  int M, N, K;
+  void* out;  // RESID: f32 [M, ldo] (+=); GELU/STORE: T [M, ldo]
+  long ldo;
+  // QKV scatter into the paged cache
+  void* q_out;            // T [M, E]
+  void* kc;               // T pool: [pages][H][16][64] for this layer
+  void* vc;
+  const int* page_table;  // [seq][maxp]
+  int maxp, H, S_new, past;
+  // logits: processors + per-workgroup argmax partials
+  float* logits_raw;  // optional [M, N] raw logits
+  float* part_val;
+  int* part_idx;
+  int nblk;
+  const int* hist;  // [M][hist_ld] generated tokens
+  int hist_ld, gen_len;
+  const int* banned;  // [M][hist_ld]
+  const int* nbanned;
+  float rep_penalty;
+  int min_new, eos;
+};
+
+hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
+                              long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s);
+int vcap_gemm_k_align(int in_dt);
+hipError_t vcap_layernorm_dispatch(int out_dt, const float* x, long ldx, void* y, long ldy, const float* gamma,
+                                   const float* beta, int rows, int D, float eps, hipStream_t s);
+hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s);
+hipError_t vcap_patchify_dispatch(int dt, const float* frames, void* patches, float* x, const float* cls,
+                                  const float* pos, int BT, int img, int p, int Kp, int N, int D, hipStream_t s);
+hipError_t vcap_vit_head_prefix_dispatch(const float* x, int B, int T, int N, int D, const float* ng, const float* nb,
+                                         float neps, const float* pw, const float* pb, int VD, float ln_scale,
+                                         float in_weight, const float* mw, const float* mb, int MO, float* enc_out,
+                                         float* prefix, const float* emb_in, hipStream_t s);
+hipError_t vcap_vit_pool_dispatch(int dt, const void* x, void* y, int B, int T, int tokens, int C, int gap,
+                                  hipStream_t s);
+hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs& a, int* nblk_out, hipStream_t s);
+int vcap_logit_blocks(int V, int M);
+hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc, const void* vc, const int* pt,
+                                          int maxp, void* out, int M, int H, int S_new, int past, hipStream_t s);
+hipError_t vcap_prefill_embed_dispatch(int dt, const float* prefix, int P, const int* ids, int nids, const void* wte,
+                                       const float* wpe, float* h, int B, int E, hipStream_t s);
+hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s);
+hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const int* part_idx, int nblk, int B,
+                                         int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
+                                         int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,
+                                         const float* wpe, float* h, int E, int pos_next, hipStream_t s);

@@ -1,0 +1,181 @@
+// ViT multi-head self-attention core: O = softmax(Q K^T / sqrt(64)) V per (frame, head).
+// Replaces timm Attention with fused_attn=True -> F.scaled_dot_product_attention
+// (src/models/video_encoder.py:112-121; no mask, no causal, scale head_dim^-0.5).
+//
+// One workgroup (4 waves) per (frame, head).  K and V of the head are staged once in LDS:
+// K row-major [NP][64] with an XOR chunk swizzle (conflict-free ds_read_b128 fragment
+// reads), V transposed to Vt[64][NP+pad].  Each wave owns 16-query tiles and computes
+// S^T = K Q^T on MFMA so a lane ends up holding 4 consecutive keys of ONE query per key
+// tile; the whole row (NP <= 288 keys) stays in registers, so softmax is exact (no online
+// rescale): row max/sum reduce over the 4 lane groups with two xor-shuffles.  The
+// accumulators are then consumed in place as the P^T operand of O^T = Vt P^T (the k
+// index permutation is applied identically to the Vt fragment), and a lane writes 4
+// consecutive head-dims of one query row.
+#include "vcap_common.h"
+#include "vcap_kernels.h"
+
+template <typename T, int KT>
+__global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                                 int N, int H) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int E = Frag<T>::kElems;     // elements per 16-byte chunk
+  constexpr int CH = 64 / E;             // chunks per 64-dim row (8 bf16, 16 f32)
+  constexpr int NP = KT * 16;            // padded key count
+  constexpr int VS = NP + (sizeof(T) == 2 ? 8 : 4);  // Vt row stride (elements)
+  constexpr int NS = 64 / (4 * E);       // 4-chunk k-slabs per 64 dims (2 bf16, 4 f32)
+  static_assert(sizeof(T) == 4 || (KT % 2) == 0, "bf16 path consumes 32-key chunks");
+
+  const int bh = blockIdx.x;
+  const int bt = bh / H, h = bh % H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const T* base = qkv + (long)bt * N * ld + h * 64;
+
+  char* Ks = smem;
+  T* Vt = reinterpret_cast<T*>(smem + NP * 64 * sizeof(T));
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // ---- stage K (swizzled) and V^T
+  for (int idx = tid; idx < NP * CH; idx += 256) {
+    const int key = idx / CH, c = idx % CH;
+    u32x4 kv = (u32x4){0u, 0u, 0u, 0u}, vv = (u32x4){0u, 0u, 0u, 0u};
+    if (key < N) {
+      kv = *reinterpret_cast<const u32x4*>(base + (long)key * ld + D + c * E);
+      vv = *reinterpret_cast<const u32x4*>(base + (long)key * ld + 2 * D + c * E);
+    }
+    *reinterpret_cast<u32x4*>(Ks + key * 64 * sizeof(T) + ((c ^ (key & (CH - 1))) << 4)) = kv;
+    const T* ve = reinterpret_cast<const T*>(&vv);
+#pragma unroll
+    for (int e = 0; e < E; ++e) Vt[(c * E + e) * VS + key] = ve[e];
+  }
+  __syncthreads();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int qtiles = (N + 15) / 16;
+  const float scale = 0.125f;  // 64^-0.5
+  for (int qt = wave; qt < qtiles; qt += 4) {
+    int q = qt * 16 + fr;
+    const int qc = q < N ? q : N - 1;
+    u32x4 qf[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[s] = *reinterpret_cast<const u32x4*>(base + (long)qc * ld + (s * 4 + fg) * E);
+
+    f32x4 st[KT];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const int key = kt * 16 + fr;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const int c = s * 4 + fg;
+        const u32x4 kf = *reinterpret_cast<const u32x4*>(Ks + key * 64 * sizeof(T) + ((c ^ (key & (CH - 1))) << 4));
+        acc = mfma_frag(kf, qf[s], acc, (T*)nullptr);
+      }
+      st[kt] = acc;  // S^T[key = kt*16 + 4*fg + r][query = fr]
+    }
+    // ---- exact softmax over the full key row of query fr
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * 16 + fg * 4 + r;
+        if (key >= N) st[kt][r] = -INFINITY;
+        mx = fmaxf(mx, st[kt][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __expf((st[kt][r] - mx) * scale);
+        st[kt][r] = p;
+        sum += p;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.0f / sum;
+
+    // ---- O^T[d][q] = sum_key Vt[d][key] * P^T[key][q]
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int c = 0; c < KT / 2; ++c) {
+        const u32x4 pf = (u32x4){pack_bf2(st[2 * c][0], st[2 * c][1]), pack_bf2(st[2 * c][2], st[2 * c][3]),
+                                 pack_bf2(st[2 * c + 1][0], st[2 * c + 1][1]),
+                                 pack_bf2(st[2 * c + 1][2], st[2 * c + 1][3])};
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const T* vrow = Vt + (dt * 16 + fr) * VS + 32 * c + 4 * fg;
+          const u32x2 lo = *reinterpret_cast<const u32x2*>(vrow);
+          const u32x2 hi = *reinterpret_cast<const u32x2*>(vrow + 16);
+          const u32x4 vf = (u32x4){lo.x, lo.y, hi.x, hi.y};
+          o[dt] = mfma_frag(vf, pf, o[dt], (T*)nullptr);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const u32x4 pf = (u32x4){__float_as_uint(st[t][0]), __float_as_uint(st[t][1]), __float_as_uint(st[t][2]),
+                                 __float_as_uint(st[t][3])};
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const u32x4 vf = *reinterpret_cast<const u32x4*>(Vt + (dt * 16 + fr) * VS + 16 * t + 4 * fg);
+          o[dt] = mfma_frag(vf, pf, o[dt], (T*)nullptr);
+        }
+      }
+    }
+    if (q < N) {
+      T* orow = out + ((long)bt * N + q) * D + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const f32x4 v = o[dt] * inv;  // O^T[d = dt*16 + 4*fg + r][q]
+        if constexpr (sizeof(T) == 2) {
+          *reinterpret_cast<u32x2*>(orow + dt * 16 + 4 * fg) = (u32x2){pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
+        } else {
+          *reinterpret_cast<f32x4*>(orow + dt * 16 + 4 * fg) = v;
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int KT>
+static hipError_t launch_attn(const void* qkv, void* out, int BT, int N, int H, hipStream_t s) {
+  constexpr int NP = KT * 16;
+  constexpr int VS = NP + (sizeof(T) == 2 ? 8 : 4);
+  const size_t lds = (size_t)NP * 64 * sizeof(T) + (size_t)64 * VS * sizeof(T);
+  static bool configured = false;  // dynamic LDS above 64 KiB needs the explicit opt-in
+  if (!configured) {
+    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_kernel<T, KT>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    configured = true;
+  }
+  hipLaunchKernelGGL((vcap_vit_attention_kernel<T, KT>), dim3(BT * H), dim3(256), lds, s, (const T*)qkv, (T*)out, N,
+                     H);
+  return hipGetLastError();
+}
+
+hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s) {
+  if (N <= 0 || N > 288) return hipErrorInvalidValue;
+  const int kt = ((N + 31) / 32) * 2;  // keys padded to a multiple of 32
+  if (dt == VCAP_DT_BF16) {
+    switch (kt) {
+      case 2: return launch_attn<bf16_t, 2>(qkv, out, BT, N, H, s);
+      case 14: return launch_attn<bf16_t, 14>(qkv, out, BT, N, H, s);
+      case 18: return launch_attn<bf16_t, 18>(qkv, out, BT, N, H, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  switch (kt) {
+    case 2: return launch_attn<float, 2>(qkv, out, BT, N, H, s);
+    case 14: return launch_attn<float, 14>(qkv, out, BT, N, H, s);
+    case 18: return launch_attn<float, 18>(qkv, out, BT, N, H, s);
+    default: return hipErrorInvalidValue;
+  }
+}

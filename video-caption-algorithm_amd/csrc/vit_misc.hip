@@ -1,0 +1,204 @@
+// ViT prologue/epilogue kernels around the block GEMMs.
+//
+//  * vcap_patchify: frames [BT,3,H,W] f32 -> im2col patches [BT*P, Kp] (T, zero K-pad) feeding the
+//    patch-embed GEMM (timm PatchEmbed Conv2d(3,D,p,stride p), called at
+//    src/models/video_encoder.py:195), and the class-token rows x[bt,0,:] = cls + pos[0]
+//    (timm _pos_embed).  The GEMM epilogue adds bias + pos[1+p] and scatters rows bt*N+1+p.
+//  * vcap_vit_head_prefix: the fused tail of the encoder + engine prefix:
+//    final LayerNorm on CLS rows only (the only rows consumed) -> mean over T
+//    (video_encoder.py:256-258) -> encoder.proj Linear D->256 (:316) -> optional
+//    layer_norm(no affine)*ln_scale*in_weight (core/engine.py:44-50) -> mapper Linear
+//    256->P*E (text_decoder.py:249).  fp32 throughout (video_encoder.py:323-324 casts to fp32).
+//  * vcap_vit_pool: the reference CuPy pool op (core/operators/cupy_vit_pool.py:23-104):
+//    y[b,c] = mean_t x[b*T+t, 0, c] ("cls") or mean_{t,p>=1} x[b*T+t, p, c] ("gap").
+#include "vcap_common.h"
+#include "vcap_kernels.h"
+
+template <typename T>
+__global__ __launch_bounds__(256) void vcap_patchify_kernel(const float* __restrict__ frames, T* __restrict__ patches,
+                                                            float* __restrict__ x, const float* __restrict__ cls,
+                                                            const float* __restrict__ pos, int BT, int img, int p,
+                                                            int Kp, int N, int D) {
+  const int g = img / p, P = g * g;
+  const int row = blockIdx.x;
+  if (row >= BT * P) {  // class-token row
+    const int bt = row - BT * P;
+    float* xr = x + (long)bt * N * D;
+    for (int d = threadIdx.x; d < D; d += 256) xr[d] = cls[d] + pos[d];
+    return;
+  }
+  const int bt = row / P, pp = row % P;
+  const int py = pp / g, px = pp % g;
+  const float* f = frames + (long)bt * 3 * img * img;
+  T* out = patches + (long)row * Kp;
+  const int K = 3 * p * p;
+  for (int k = threadIdx.x; k < Kp; k += 256) {
+    float v = 0.f;
+    if (k < K) {
+      const int c = k / (p * p), rem = k % (p * p), i = rem / p, j = rem % p;
+      v = f[((long)c * img + (py * p + i)) * img + (px * p + j)];
+    }
+    out[k] = Num<T>::from_f(v);
+  }
+}
+
+hipError_t vcap_patchify_dispatch(int dt, const float* frames, void* patches, float* x, const float* cls,
+                                  const float* pos, int BT, int img, int p, int Kp, int N, int D, hipStream_t s) {
+  const int g = img / p;
+  const dim3 grid(BT * g * g + BT), block(256);
+  if (dt == VCAP_DT_BF16)
+    hipLaunchKernelGGL((vcap_patchify_kernel<bf16_t>), grid, block, 0, s, frames, (bf16_t*)patches, x, cls, pos, BT,
+                       img, p, Kp, N, D);
+  else
+    hipLaunchKernelGGL((vcap_patchify_kernel<float>), grid, block, 0, s, frames, (float*)patches, x, cls, pos, BT,
+                       img, p, Kp, N, D);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+constexpr int HEAD_CHUNK = 256;  // mapper outputs per block
+
+__global__ __launch_bounds__(256) void vcap_vit_head_prefix_kernel(
+    const float* __restrict__ x, int T, int N, int D, const float* __restrict__ ng, const float* __restrict__ nb,
+    float neps, const float* __restrict__ pw, const float* __restrict__ pb, int VD, float ln_scale, float in_weight,
+    const float* __restrict__ mw, const float* __restrict__ mb, int MO, float* __restrict__ enc_out,
+    float* __restrict__ prefix, const float* __restrict__ emb_in) {
+  __shared__ float part[4][1024];
+  __shared__ float pooled[1024];
+  __shared__ float emb[1024];
+  const int b = blockIdx.x, chunk = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  if (emb_in) {  // vcap_prefix_project: start from a given encoder output
+    for (int o = tid; o < VD; o += 256) emb[o] = emb_in[(long)b * VD + o];
+    __syncthreads();
+    goto prefix_norm;
+  }
+  {
+  // 1) final LayerNorm of each frame's CLS row, summed over frames (per-wave partials)
+  float accv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) accv[i] = 0.f;
+  for (int t = wave; t < T; t += 4) {
+    const float* xr = x + ((long)(b * T + t) * N) * D;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) s += xr[c];
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) {
+        const float d = xr[c] - mean;
+        ss += d * d;
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)D + neps);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = lane + 64 * i;
+      if (c < D) accv[i] += (xr[c] - mean) * rstd * ng[c] + nb[c];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = lane + 64 * i;
+    if (c < D) part[wave][c] = accv[i];
+  }
+  __syncthreads();
+  for (int c = tid; c < D; c += 256) pooled[c] = (part[0][c] + part[1][c] + part[2][c] + part[3][c]) / (float)T;
+  __syncthreads();
+
+  // 2) encoder.proj: emb[o] = pooled . pw[o] + pb[o]
+  for (int o = wave; o < VD; o += 4) {
+    const float* w = pw + (long)o * D;
+    float s = 0.f;
+    for (int c = lane; c < D; c += 64) s += pooled[c] * w[c];
+    s = wave_sum(s);
+    if (lane == 0) emb[o] = s + pb[o];
+  }
+  __syncthreads();
+  if (chunk == 0 && enc_out)
+    for (int o = tid; o < VD; o += 256) enc_out[(long)b * VD + o] = emb[o];
+  }
+prefix_norm:
+  if (!prefix) return;
+
+  // 3) engine prefix normalisation (layer_norm without affine, eps 1e-5) * ln_scale, * in_weight
+  if (ln_scale > 0.f || in_weight > 0.f) {
+    if (wave == 0) {
+      float s = 0.f;
+      for (int c = lane; c < VD; c += 64) s += emb[c];
+      const float mean = wave_sum(s) / (float)VD;
+      float ss = 0.f;
+      for (int c = lane; c < VD; c += 64) {
+        const float d = emb[c] - mean;
+        ss += d * d;
+      }
+      const float rstd = rsqrtf(wave_sum(ss) / (float)VD + 1e-5f);
+      for (int c = lane; c < VD; c += 64) {
+        float v = emb[c];
+        if (ln_scale > 0.f) v = (v - mean) * rstd * ln_scale;
+        if (in_weight > 0.f) v = v * in_weight;
+        emb[c] = v;
+      }
+    }
+    __syncthreads();
+  }
+
+  // 4) mapper rows [chunk*HEAD_CHUNK, +HEAD_CHUNK)
+  const int o0 = chunk * HEAD_CHUNK;
+  for (int o = o0 + wave; o < o0 + HEAD_CHUNK && o < MO; o += 4) {
+    const float* w = mw + (long)o * VD;
+    float s = 0.f;
+    for (int c = lane; c < VD; c += 64) s += emb[c] * w[c];
+    s = wave_sum(s);
+    if (lane == 0) prefix[(long)b * MO + o] = s + mb[o];
+  }
+}
+
+hipError_t vcap_vit_head_prefix_dispatch(const float* x, int B, int T, int N, int D, const float* ng, const float* nb,
+                                         float neps, const float* pw, const float* pb, int VD, float ln_scale,
+                                         float in_weight, const float* mw, const float* mb, int MO, float* enc_out,
+                                         float* prefix, const float* emb_in, hipStream_t s) {
+  if (D > 1024 || VD > 1024) return hipErrorInvalidValue;
+  const int chunks = prefix ? (MO + HEAD_CHUNK - 1) / HEAD_CHUNK : 1;
+  const dim3 grid(B, chunks), block(256);
+  hipLaunchKernelGGL(vcap_vit_head_prefix_kernel, grid, block, 0, s, x, T, N, D, ng, nb, neps, pw, pb, VD, ln_scale,
+                     in_weight, mw, mb, MO, enc_out, prefix, emb_in);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void vcap_vit_pool_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int Tn,
+                                                            int tokens, int C, int gap) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * C) return;
+  const int b = idx / C, c = idx % C;
+  float acc = 0.f;
+  if (!gap) {
+    for (int t = 0; t < Tn; ++t) acc += Num<T>::to_f(x[((long)(b * Tn + t) * tokens) * C + c]);
+    y[idx] = Num<T>::from_f(acc / (float)Tn);
+  } else {
+    for (int t = 0; t < Tn; ++t)
+      for (int p = 1; p < tokens; ++p) acc += Num<T>::to_f(x[((long)(b * Tn + t) * tokens + p) * C + c]);
+    y[idx] = Num<T>::from_f(acc / (float)(Tn * (tokens - 1)));
+  }
+}
+
+hipError_t vcap_vit_pool_dispatch(int dt, const void* x, void* y, int B, int T, int tokens, int C, int gap,
+                                  hipStream_t s) {
+  const dim3 grid((B * C + 255) / 256), block(256);
+  if (dt == VCAP_DT_BF16)
+    hipLaunchKernelGGL((vcap_vit_pool_kernel<bf16_t>), grid, block, 0, s, (const bf16_t*)x, (bf16_t*)y, B, T, tokens,
+                       C, gap);
+  else
+    hipLaunchKernelGGL((vcap_vit_pool_kernel<float>), grid, block, 0, s, (const float*)x, (float*)y, B, T, tokens, C,
+                       gap);
+  return hipGetLastError();
+}

@@ -1,0 +1,116 @@
+"""ctypes binding of the C ABI in include/vcap.h (libvcap_hip.so).
+
+The library is the only compute path of the product: there is no torch or CPU fallback.
+If the shared object is missing or fails to load, `lib()` raises; callers never route
+around it.  The CuPy operators of the reference kept a torch fallback with
+`last_backend`/`last_error` bookkeeping (core/operators/cupy_linear_mapper.py:168-184);
+here a failing call raises `VcapError` carrying vcap_last_error().
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
+_lib = None
+
+DT_F32, DT_BF16 = 0, 1
+ABI_VERSION = 1
+
+vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
+fp = C.POINTER(C.c_float)
+
+
+class VcapError(RuntimeError):
+    pass
+
+
+class VitLayer(C.Structure):
+    _fields_ = [("ln1_g", vp), ("ln1_b", vp), ("qkv_w", vp), ("qkv_b", vp), ("proj_w", vp), ("proj_b", vp),
+                ("ln2_g", vp), ("ln2_b", vp), ("fc1_w", vp), ("fc1_b", vp), ("fc2_w", vp), ("fc2_b", vp)]
+
+
+class VitDesc(C.Structure):
+    _fields_ = [("dtype", i32), ("dim", i32), ("depth", i32), ("heads", i32), ("patch", i32), ("image", i32),
+                ("mlp", i32), ("video_dim", i32), ("kpad", i32), ("ln_eps", f32), ("patch_w", vp),
+                ("patch_b", vp), ("cls", vp), ("pos", vp), ("norm_g", vp), ("norm_b", vp), ("proj_w", vp),
+                ("proj_b", vp), ("layers", C.POINTER(VitLayer))]
+
+
+class PrefixDesc(C.Structure):
+    _fields_ = [("ln_scale", f32), ("in_weight", f32), ("prefix_len", i32), ("n_embd", i32), ("mapper_w", vp),
+                ("mapper_b", vp)]
+
+
+class GPT2Layer(C.Structure):
+    _fields_ = [("ln1_g", vp), ("ln1_b", vp), ("attn_w", vp), ("attn_b", vp), ("aproj_w", vp), ("aproj_b", vp),
+                ("ln2_g", vp), ("ln2_b", vp), ("fc_w", vp), ("fc_b", vp), ("mproj_w", vp), ("mproj_b", vp)]
+
+
+class GPT2Desc(C.Structure):
+    _fields_ = [("dtype", i32), ("n_embd", i32), ("n_layer", i32), ("n_head", i32), ("vocab", i32),
+                ("n_positions", i32), ("prefix_len", i32), ("ln_eps", f32), ("wte", vp), ("wpe", vp),
+                ("lnf_g", vp), ("lnf_b", vp), ("layers", C.POINTER(GPT2Layer))]
+
+
+class GenParams(C.Structure):
+    _fields_ = [("max_new_tokens", i32), ("min_new_tokens", i32), ("no_repeat_ngram_size", i32),
+                ("repetition_penalty", f32), ("eos_token_id", i32), ("pad_token_id", i32), ("use_graph", i32)]
+
+
+# name -> (restype, argtypes); every symbol include/vcap.h declares
+SIGNATURES = {
+    "vcap_last_error": (C.c_char_p, []),
+    "vcap_abi_version": (i32, []),
+    "vcap_linear_bias": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, vp]),
+    "vcap_gemm": (i32, [i32, i32, vp, i64, vp, i64, vp, i64, i32, i32, i32, vp, i32, vp, i64, i32, i32, i32, i32,
+                        i32, vp]),
+    "vcap_layernorm": (i32, [i32, vp, i64, vp, i64, vp, vp, i32, i32, f32, vp]),
+    "vcap_vit_attention": (i32, [i32, vp, vp, i32, i32, i32, vp]),
+    "vcap_vit_pool_temporal": (i32, [i32, vp, vp, i32, i32, i32, i32, i32, vp]),
+    "vcap_prefix_project": (i32, [vp, i32, i32, C.POINTER(PrefixDesc), vp, vp]),
+    "vcap_vit_workspace_bytes": (sz, [C.POINTER(VitDesc), i32, i32]),
+    "vcap_vit_encode": (i32, [C.POINTER(VitDesc), C.POINTER(PrefixDesc), vp, i32, i32, vp, vp, vp, sz, vp]),
+    "vcap_gpt2_workspace_bytes": (sz, [C.POINTER(GPT2Desc), i32, i32, i32]),
+    "vcap_gpt2_generate": (i32, [C.POINTER(GPT2Desc), C.POINTER(GenParams), vp, C.POINTER(C.c_int), i32, i32, vp,
+                                 vp, vp, sz, vp]),
+    "vcap_graph_cache_clear": (None, []),
+    "vcap_probe_enable": (i32, [C.c_char_p, i32]),
+    "vcap_probe_read": (i32, [C.c_char_p, fp, C.POINTER(C.c_int)]),
+}
+
+
+def library_path() -> Path:
+    return Path(os.environ.get("VCAP_LIB", str(_LIB_PATH)))
+
+
+def lib():
+    """Load libvcap_hip.so once; raise if it is absent (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    if not path.exists():
+        raise VcapError(f"libvcap_hip.so not built at {path}; run `python -m vcap.build` "
+                        "(or __graft_entry__.build()) - the HIP path has no CPU fallback")
+    h = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(h, name)
+        fn.restype = res
+        fn.argtypes = args
+    if h.vcap_abi_version() != ABI_VERSION:
+        raise VcapError(f"ABI mismatch: library {h.vcap_abi_version()} vs binding {ABI_VERSION}")
+    _lib = h
+    return h
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().vcap_last_error()
+        raise VcapError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t) -> int:
+    """Raw device address of a torch tensor (None -> NULL)."""
+    return 0 if t is None else t.data_ptr()

@@ -1,0 +1,285 @@
+"""Device-resident ViT encoder and GPT-2 decoder driven through the C ABI.
+
+`HipViTEncoder` and `HipGPT2Decoder` own the packed weights in HBM (operand dtype bf16 for
+throughput or fp32 for the parity mode), build the include/vcap.h descriptors once, keep a
+reusable workspace, and issue one ABI call per encode / per whole decode.
+
+Weight packing from the reference's state-dict layout:
+  * ViT Linear weights keep torch's [out, in] layout (K contiguous), the patch-embed conv
+    weight is flattened to [D, 3*p*p] and zero-padded in K to the GEMM K step;
+  * GPT-2 Conv1D weights ([in, out], x @ W + b) are transposed to [out, in];
+  * wte is shared by the embedding lookup and the tied lm_head (text_decoder.py:28);
+  * LayerNorm affines, biases, positional tables, encoder.proj and the mapper stay fp32.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .configs import VIDEO_DIM, GPT2Arch, ViTArch
+
+_DTYPES = {"bf16": (N.DT_BF16, torch.bfloat16), "fp32": (N.DT_F32, torch.float32)}
+
+
+def _dtype(mode: str):
+    if mode not in _DTYPES:
+        raise ValueError(f"precision must be one of {sorted(_DTYPES)}, got {mode!r}")
+    return _DTYPES[mode]
+
+
+def _stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class _Workspace:
+    def __init__(self, device):
+        self.device = device
+        self.buf: Optional[torch.Tensor] = None
+
+    def get(self, nbytes: int) -> torch.Tensor:
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+        return self.buf
+
+
+class HipViTEncoder:
+    """ViTFrameEncoder.forward (src/models/video_encoder.py:288-326) on the HIP path."""
+
+    def __init__(self, sd: Dict[str, np.ndarray], arch: ViTArch, precision: str = "bf16", device="cuda",
+                 video_dim: int = VIDEO_DIM):
+        N.lib()
+        self.arch, self.precision, self.device = arch, precision, torch.device(device)
+        self.dt, tdt = _dtype(precision)
+        self.video_dim = video_dim
+        p = "encoder.backbone."
+        dev = self.device
+
+        def f32(k, shape=None):
+            t = torch.from_numpy(np.ascontiguousarray(sd[k], dtype=np.float32))
+            if shape is not None:
+                t = t.reshape(shape)
+            return t.to(dev).contiguous()
+
+        def wt(k, shape=None):
+            return f32(k, shape).to(tdt).contiguous()
+
+        kstep = 64 if self.dt == N.DT_BF16 else 32
+        K = arch.patch_k
+        self.kpad = ((K + 63) // 64) * 64 if kstep == 64 else ((K + 31) // 32) * 32
+        pw = torch.zeros(arch.dim, self.kpad, dtype=torch.float32)
+        pw[:, :K] = torch.from_numpy(np.ascontiguousarray(sd[p + "patch_embed.proj.weight"])).reshape(arch.dim, K)
+        self._keep: List[torch.Tensor] = []
+        keep = self._keep.append
+        self.patch_w = pw.to(dev).to(tdt).contiguous()
+        keep(self.patch_w)
+        t = {
+            "patch_b": f32(p + "patch_embed.proj.bias"),
+            "cls": f32(p + "cls_token", (arch.dim,)),
+            "pos": f32(p + "pos_embed", (arch.tokens, arch.dim)),
+            "norm_g": f32(p + "norm.weight"), "norm_b": f32(p + "norm.bias"),
+            "proj_w": f32("encoder.proj.weight"), "proj_b": f32("encoder.proj.bias"),
+        }
+        for v in t.values():
+            keep(v)
+        self.layers = (N.VitLayer * arch.depth)()
+        for i in range(arch.depth):
+            b = f"{p}blocks.{i}."
+            lt = dict(ln1_g=f32(b + "norm1.weight"), ln1_b=f32(b + "norm1.bias"),
+                      qkv_w=wt(b + "attn.qkv.weight"), qkv_b=f32(b + "attn.qkv.bias"),
+                      proj_w=wt(b + "attn.proj.weight"), proj_b=f32(b + "attn.proj.bias"),
+                      ln2_g=f32(b + "norm2.weight"), ln2_b=f32(b + "norm2.bias"),
+                      fc1_w=wt(b + "mlp.fc1.weight"), fc1_b=f32(b + "mlp.fc1.bias"),
+                      fc2_w=wt(b + "mlp.fc2.weight"), fc2_b=f32(b + "mlp.fc2.bias"))
+            for k, v in lt.items():
+                keep(v)
+                setattr(self.layers[i], k, v.data_ptr())
+        self.desc = N.VitDesc(dtype=self.dt, dim=arch.dim, depth=arch.depth, heads=arch.heads, patch=arch.patch,
+                              image=arch.image, mlp=arch.mlp, video_dim=video_dim, kpad=self.kpad,
+                              ln_eps=arch.ln_eps, patch_w=self.patch_w.data_ptr(), patch_b=t["patch_b"].data_ptr(),
+                              cls=t["cls"].data_ptr(), pos=t["pos"].data_ptr(), norm_g=t["norm_g"].data_ptr(),
+                              norm_b=t["norm_b"].data_ptr(), proj_w=t["proj_w"].data_ptr(),
+                              proj_b=t["proj_b"].data_ptr(), layers=self.layers)
+        self.ws = _Workspace(dev)
+
+    def workspace_bytes(self, B: int, T: int) -> int:
+        return int(N.lib().vcap_vit_workspace_bytes(C.byref(self.desc), B, T))
+
+    def encode(self, video: torch.Tensor, prefix: Optional["HipPrefix"] = None):
+        """video [B,T,3,H,W] (or [B,3,H,W]) f32 on device -> (enc_out [B,256] f32, prefix [B,P,E] f32|None)."""
+        if video.dim() == 4:
+            video = video.unsqueeze(1)
+        if video.dim() != 5:
+            raise ValueError(f"expect [B,T,3,H,W], got {tuple(video.shape)}")
+        B, T, Cc, H, W = video.shape
+        a = self.arch
+        if Cc != 3 or H != a.image or W != a.image:
+            raise ValueError(f"expect frames of 3x{a.image}x{a.image}, got {tuple(video.shape)}")
+        if video.device != self.device and not (video.is_cuda and self.device.type == "cuda"):
+            raise ValueError("video must be on the encoder's device")
+        video = video.to(torch.float32).contiguous()
+        enc = torch.empty(B, self.video_dim, dtype=torch.float32, device=video.device)
+        pre = None
+        pd = None
+        if prefix is not None:
+            pre = torch.empty(B, prefix.prefix_len, prefix.n_embd, dtype=torch.float32, device=video.device)
+            pd = C.byref(prefix.desc)
+        nbytes = self.workspace_bytes(B, T)
+        ws = self.ws.get(nbytes)
+        N.check(N.lib().vcap_vit_encode(C.byref(self.desc), pd, video.data_ptr(), B, T, enc.data_ptr(),
+                                        N.ptr(pre), ws.data_ptr(), ws.numel(), _stream(video.device)),
+                "vcap_vit_encode")
+        return enc, pre
+
+
+class HipPrefix:
+    """Engine prefix normalisation (core/engine.py:44-50) + mapper (text_decoder.py:249)."""
+
+    def __init__(self, sd: Dict[str, np.ndarray], n_embd: int, prefix_len: int = 4, ln_scale: float = 0.6,
+                 in_weight: float = 0.4, device="cuda"):
+        dev = torch.device(device)
+        self.prefix_len, self.n_embd = prefix_len, n_embd
+        self.mapper_w = torch.from_numpy(np.ascontiguousarray(sd["decoder.mapper.0.weight"], np.float32)).to(dev)
+        self.mapper_b = torch.from_numpy(np.ascontiguousarray(sd["decoder.mapper.0.bias"], np.float32)).to(dev)
+        if self.mapper_w.shape[0] != prefix_len * n_embd:
+            raise ValueError(f"mapper out {self.mapper_w.shape[0]} != prefix_len*n_embd {prefix_len * n_embd}")
+        self.set_scales(ln_scale, in_weight)
+
+    def set_scales(self, ln_scale: Optional[float], in_weight: Optional[float]) -> None:
+        self.ln_scale = float(ln_scale) if ln_scale is not None else 0.0
+        self.in_weight = float(in_weight) if in_weight is not None else 0.0
+        self.desc = N.PrefixDesc(ln_scale=self.ln_scale, in_weight=self.in_weight, prefix_len=self.prefix_len,
+                                 n_embd=self.n_embd, mapper_w=self.mapper_w.data_ptr(),
+                                 mapper_b=self.mapper_b.data_ptr())
+
+    def project(self, emb: torch.Tensor) -> torch.Tensor:
+        """emb [B,256] or [B,1,256] f32 -> prefix embeds [B, P, E] (vcap_prefix_project)."""
+        B = emb.shape[0]
+        e = emb.reshape(B, -1).to(torch.float32).contiguous()
+        out = torch.empty(B, self.prefix_len, self.n_embd, dtype=torch.float32, device=e.device)
+        N.check(N.lib().vcap_prefix_project(e.data_ptr(), B, e.shape[1], C.byref(self.desc), out.data_ptr(),
+                                            _stream(e.device)), "vcap_prefix_project")
+        return out
+
+
+@dataclass
+class GenConfig:
+    max_new_tokens: int = 24
+    min_new_tokens: int = 8
+    no_repeat_ngram_size: int = 3
+    repetition_penalty: float = 1.1
+    eos_token_id: int = 50256
+    pad_token_id: int = 50256
+    use_graph: bool = True
+
+    @classmethod
+    def raw_greedy(cls, max_new_tokens: int = 24, eos: int = 50256, use_graph: bool = True) -> "GenConfig":
+        """benchmark_baseline.run_decoder_steps semantics: argmax, no processors, no min length."""
+        return cls(max_new_tokens, 0, 0, 1.0, eos, eos, use_graph)
+
+
+class HipGPT2Decoder:
+    """GPT2LMHeadModel greedy generate from inputs_embeds (text_decoder.py:131-144) on the HIP path."""
+
+    def __init__(self, sd: Dict[str, np.ndarray], arch: GPT2Arch, precision: str = "bf16", device="cuda",
+                 prefix_len: int = 4):
+        N.lib()
+        self.arch, self.precision, self.device = arch, precision, torch.device(device)
+        self.dt, tdt = _dtype(precision)
+        self.prefix_len = prefix_len
+        dev = self.device
+        p = "decoder.model.transformer."
+        self._keep: List[torch.Tensor] = []
+
+        def f32(k):
+            t = torch.from_numpy(np.ascontiguousarray(sd[k], dtype=np.float32)).to(dev).contiguous()
+            self._keep.append(t)
+            return t
+
+        def conv_t(k):  # Conv1D [in, out] -> [out, in]
+            t = torch.from_numpy(np.ascontiguousarray(sd[k], dtype=np.float32)).t().contiguous()
+            t = t.to(dev).to(tdt).contiguous()
+            self._keep.append(t)
+            return t
+
+        self.wte = torch.from_numpy(np.ascontiguousarray(sd[p + "wte.weight"], np.float32)).to(dev).to(tdt)
+        self.wte = self.wte.contiguous()
+        self._keep.append(self.wte)
+        self.wpe = f32(p + "wpe.weight")
+        lnf_g, lnf_b = f32(p + "ln_f.weight"), f32(p + "ln_f.bias")
+        self.layers = (N.GPT2Layer * arch.n_layer)()
+        for i in range(arch.n_layer):
+            b = f"{p}h.{i}."
+            ly = self.layers[i]
+            ly.ln1_g, ly.ln1_b = f32(b + "ln_1.weight").data_ptr(), f32(b + "ln_1.bias").data_ptr()
+            ly.attn_w, ly.attn_b = conv_t(b + "attn.c_attn.weight").data_ptr(), f32(b + "attn.c_attn.bias").data_ptr()
+            ly.aproj_w = conv_t(b + "attn.c_proj.weight").data_ptr()
+            ly.aproj_b = f32(b + "attn.c_proj.bias").data_ptr()
+            ly.ln2_g, ly.ln2_b = f32(b + "ln_2.weight").data_ptr(), f32(b + "ln_2.bias").data_ptr()
+            ly.fc_w, ly.fc_b = conv_t(b + "mlp.c_fc.weight").data_ptr(), f32(b + "mlp.c_fc.bias").data_ptr()
+            ly.mproj_w = conv_t(b + "mlp.c_proj.weight").data_ptr()
+            ly.mproj_b = f32(b + "mlp.c_proj.bias").data_ptr()
+        self.desc = N.GPT2Desc(dtype=self.dt, n_embd=arch.n_embd, n_layer=arch.n_layer, n_head=arch.n_head,
+                               vocab=arch.vocab, n_positions=arch.n_positions, prefix_len=prefix_len,
+                               ln_eps=arch.ln_eps, wte=self.wte.data_ptr(), wpe=self.wpe.data_ptr(),
+                               lnf_g=lnf_g.data_ptr(), lnf_b=lnf_b.data_ptr(), layers=self.layers)
+        self.ws = _Workspace(dev)
+
+    def workspace_bytes(self, B: int, prompt_len: int, max_new: int) -> int:
+        return int(N.lib().vcap_gpt2_workspace_bytes(C.byref(self.desc), B, self.prefix_len + prompt_len, max_new))
+
+    def generate_ids(self, prefix: torch.Tensor, prompt_ids: Sequence[int], cfg: GenConfig,
+                     out: Optional[torch.Tensor] = None, logits_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """prefix [B,P,E] f32 device, prompt ids (BOS-only prompt = [eos]) -> int32 [B, max_new] EOS-padded."""
+        B, P, E = prefix.shape
+        if P != self.prefix_len or E != self.arch.n_embd:
+            raise ValueError(f"prefix shape {tuple(prefix.shape)} != [B,{self.prefix_len},{self.arch.n_embd}]")
+        prefix = prefix.to(torch.float32).contiguous()
+        ids = list(int(i) for i in prompt_ids)
+        mx = int(cfg.max_new_tokens)
+        if out is None:
+            out = torch.empty(B, mx, dtype=torch.int32, device=prefix.device)
+        if logits_out is not None and tuple(logits_out.shape) != (mx, B, self.arch.vocab):
+            raise ValueError("logits_out must be [max_new, B, vocab] f32")
+        gp = N.GenParams(max_new_tokens=mx, min_new_tokens=int(cfg.min_new_tokens),
+                         no_repeat_ngram_size=int(cfg.no_repeat_ngram_size),
+                         repetition_penalty=float(cfg.repetition_penalty), eos_token_id=int(cfg.eos_token_id),
+                         pad_token_id=int(cfg.pad_token_id), use_graph=int(bool(cfg.use_graph)))
+        arr = (C.c_int * max(len(ids), 1))(*ids)
+        ws = self.ws.get(self.workspace_bytes(B, len(ids), mx))
+        N.check(N.lib().vcap_gpt2_generate(C.byref(self.desc), C.byref(gp), prefix.data_ptr(), arr, len(ids), B,
+                                           out.data_ptr(), N.ptr(logits_out), ws.data_ptr(), ws.numel(),
+                                           _stream(prefix.device)), "vcap_gpt2_generate")
+        return out
+
+
+def trim_generated(ids: torch.Tensor, eos: int) -> List[List[int]]:
+    """HF generate output length: it stops after the first step where every row has finished
+    (generation/utils.py stopping criteria); rows finished earlier are EOS-padded."""
+    a = ids.cpu().numpy()
+    B, L = a.shape
+    fin = np.zeros(B, dtype=bool)
+    stop = L
+    for s in range(L):
+        fin |= a[:, s] == eos
+        if fin.all():
+            stop = s + 1
+            break
+    return [list(map(int, a[b, :stop])) for b in range(B)]
+
+
+def raw_greedy_tokens(ids: torch.Tensor, eos: int) -> List[List[int]]:
+    """benchmark_baseline.run_decoder_steps bookkeeping: tokens up to and including the first EOS."""
+    out = []
+    for row in ids.cpu().numpy().tolist():
+        toks = []
+        for t in row:
+            toks.append(int(t))
+            if t == eos:
+                break
+        out.append(toks)
+    return out

@@ -130,6 +130,20 @@ int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const
                        void* stream);
 void vcap_graph_cache_clear(void);
 
+/* ---- step-wise decode for host-driven search (beam search / sampling).  One state carved for
+ *      `rows` decoder rows lives in the caller's workspace across calls:
+ *        prefill  B <= rows sequences into rows [0, B), logits of each last position -> [B, vocab]
+ *        step     feed one token per row at position `pos` (S0 <= pos < S0+max_new) -> [rows, vocab]
+ *        reorder  row r <- row src_rows[r] for cache positions [0, length)   (beam reordering,
+ *                 also the B -> B*num_beams expansion after prefill) ---- */
+size_t vcap_gpt2_beam_workspace_bytes(const vcap_gpt2_desc* d, int rows, int S0, int max_new_tokens);
+int vcap_gpt2_prefill(const vcap_gpt2_desc* d, const float* prefix, const int* prompt_ids, int prompt_len, int B,
+                      int rows, int max_new_tokens, float* logits_out, void* workspace, size_t ws_bytes, void* stream);
+int vcap_gpt2_step(const vcap_gpt2_desc* d, const int* tokens, int rows, int S0, int max_new_tokens, int pos,
+                   float* logits_out, void* workspace, size_t ws_bytes, void* stream);
+int vcap_gpt2_reorder(const vcap_gpt2_desc* d, const int* src_rows, int rows, int S0, int max_new_tokens, int length,
+                      void* workspace, size_t ws_bytes, void* stream);
+
 /* ---- live kernel timing for the benchmark's roofline (sites: "vit.qkv", "vit.attention",
  *      "vit.proj", "vit.fc1", "vit.fc2"): events are recorded around each launch of the site on
  *      the caller's stream, without synchronising; vcap_probe_read waits for them. ---- */

@@ -1,0 +1,121 @@
+"""CPU suite for the drop-in surface: presets, post-processing pinned to the reference's own
+outputs (tests/golden/text_rules.json), backend switch error semantics, tokenizer, plugin
+registry, CLI flags, checkpoint key handling and the data-parallel shard/gather path (gloo, W=2)."""
+import json
+import os
+import socket
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from core.config import InferenceConfig, TensorRTConfig
+from core.inference import preset_to_kwargs
+from core.models.model_loader import load_caption_model
+from core.postprocessing.candidate_ranker import score_sentence, select_best
+from core.postprocessing.text_cleaner import clean_text
+from vcap.dist import gather_ids, shard_range
+from vcap.tokenizer import IdTokenizer
+from vcap.weights import normalize_checkpoint
+
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def test_presets_match_reference_table():
+    assert preset_to_kwargs("precise") == dict(num_beams=3, max_new_tokens=24, temperature=1.0, top_p=1.0,
+                                               no_repeat_ngram_size=3, repetition_penalty=1.1)
+    assert preset_to_kwargs("detailed")["num_beams"] == 4 and preset_to_kwargs("detailed")["max_new_tokens"] == 40
+    assert preset_to_kwargs("safe_sample")["max_new_tokens"] == 22
+    assert preset_to_kwargs(None) == preset_to_kwargs("precise") == preset_to_kwargs("unknown")
+    assert preset_to_kwargs("NATURAL")["temperature"] == 0.9
+
+
+def test_text_rules_match_reference_outputs():
+    g = json.loads((GOLD / "text_rules.json").read_text())
+    for raw, want in g["clean_text"]:
+        assert clean_text(raw) == want, raw
+    for raw, want in g["score_sentence"]:
+        assert score_sentence(raw) == pytest.approx(want, abs=1e-12)
+    texts = [t for t, _ in g["clean_text"]]
+    for (a, b, c), want in zip(zip(texts, texts[1:], texts[2:]), g["select_best"]):
+        assert list(select_best([("S1", a), ("S2", b), ("S3", c)])) == want
+
+
+def test_backend_switch_error_semantics():
+    with pytest.raises(ValueError):
+        load_caption_model(InferenceConfig(backend="torch"))
+    with pytest.raises(ValueError):
+        load_caption_model(InferenceConfig(backend="onnx"))
+    with pytest.raises(NotImplementedError):
+        load_caption_model(InferenceConfig(backend="tensorrt"))
+    with pytest.raises(NotImplementedError):
+        load_caption_model(InferenceConfig(tensorrt=TensorRTConfig(enabled=True)))
+
+
+def test_id_tokenizer_surface():
+    tok = IdTokenizer(50256)
+    assert tok("").input_ids.tolist() == [[50256]]
+    assert tok("ids:464 3290").input_ids.tolist() == [[464, 3290]]
+    assert tok.batch_decode([[464, 50256, 50256]]) == ["464"]
+    with pytest.raises(ValueError):
+        tok.encode_prompt("a natural language prompt")
+
+
+def test_checkpoint_normalisation():
+    w = np.ones((2, 2), np.float32)
+    sd = normalize_checkpoint({"model_state": {"vit.blocks.0.norm1.weight": w,
+                                               "decoder.model.transformer.wte.weight": w}})
+    assert "encoder.backbone.blocks.0.norm1.weight" in sd
+    assert sd["decoder.model.lm_head.weight"] is sd["decoder.model.transformer.wte.weight"]
+
+
+def test_plugin_registry_names_abi_symbols():
+    from core.operators.plugin_hooks import get_plugin_hook, list_plugin_hooks
+    from vcap import _native as N
+    assert get_plugin_hook("temporal_mean_pool").plugin_name == "HipTemporalMeanPool"
+    assert all(h.abi_symbol in N.SIGNATURES for h in list_plugin_hooks())
+
+
+def test_cli_flags():
+    from src.cli.inference import parse
+    a = parse(["--video_path", "clip_dir", "--num_frames", "16", "--checkpoint", "x.pt"])
+    assert a.video_path == "clip_dir" and a.num_frames == 16 and a.ckpt == "x.pt"
+
+
+@pytest.mark.parametrize("n,w", [(8, 1), (8, 2), (64, 8), (10, 4), (3, 8)])
+def test_shard_range_partitions(n, w):
+    spans = [shard_range(n, w, r) for r in range(w)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert max(e - s for s, e in spans) - min(e - s for s, e in spans) <= 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    local = torch.arange(6, dtype=torch.int32).reshape(2, 3) + 100 * rank
+    out = gather_ids(local, world)
+    q.put((rank, out.tolist()))
+    torch.distributed.destroy_process_group()
+
+
+def test_gather_ids_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    want = [[0, 1, 2], [3, 4, 5], [100, 101, 102], [103, 104, 105]]
+    assert res[0] == want and res[1] == want

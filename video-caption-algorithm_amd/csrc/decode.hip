@@ -15,105 +15,13 @@
 #include "vcap_common.h"
 #include "vcap_kernels.h"
 
-template <typename T, int MT, int NTB, int PRO, int EPI>
-__global__ __launch_bounds__(256) void vcap_rows_gemm_kernel(RowsGemmArgs a) {
-  constexpr int E = Frag<T>::kElems;
-  constexpr int KS = 4 * E;  // K per MFMA group (32 bf16 / 16 f32)
-  constexpr int U = 4;       // k-slabs of W fragments kept in flight
-  __shared__ float s_mean[MT * 16], s_rstd[MT * 16];
-  __shared__ __attribute__((aligned(16))) float red[4][MT * NTB * 256];
-  __shared__ float lg[EPI == EPI_LOGITS ? MT * 16 : 1][NTB * 16];
-
+// Split-K reduction over the 4 waves through LDS + the role's epilogue.
+template <typename T, int MT, int NTB, int EPI>
+VCAP_DEV void rows_epilogue(const RowsGemmArgs& a, f32x4 (&acc)[MT][NTB], float (*red)[MT * NTB * 256],
+                            float (*lg)[NTB * 16], int n0) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const int M = a.M, N = a.N, K = a.K;
-  const int n0 = blockIdx.x * NTB * 16;
-
-  if constexpr (PRO == PRO_LN) {
-    const float* X = (const float*)a.x;
-    for (int m = wave; m < M; m += 4) {
-      const float* xr = X + (long)m * a.ldx;
-      float s = 0.f;
-      for (int c = lane; c < K; c += 64) s += xr[c];
-      const float mean = wave_sum(s) / (float)K;
-      float ss = 0.f;
-      for (int c = lane; c < K; c += 64) {
-        const float d = xr[c] - mean;
-        ss += d * d;
-      }
-      const float var = wave_sum(ss) / (float)K;  // whole-wave reduction, outside the lane-0 branch
-      if (lane == 0) {
-        s_mean[m] = mean;
-        s_rstd[m] = rsqrtf(var + a.ln_eps);
-      }
-    }
-    __syncthreads();
-  }
-
-  f32x4 acc[MT][NTB];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NTB; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const T* W = (const T*)a.w;
-  const int kq = K / 4, kb = wave * kq, nsl = kq / KS;
-  int wrow[NTB];
-#pragma unroll
-  for (int j = 0; j < NTB; ++j) {
-    const int n = n0 + j * 16 + fr;
-    wrow[j] = n < N ? n : N - 1;
-  }
-  for (int s0 = 0; s0 < nsl; s0 += U) {
-    u32x4 wf[U][NTB];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int j = 0; j < NTB; ++j)
-        if (s0 + u < nsl)
-          wf[u][j] = __builtin_nontemporal_load(
-              reinterpret_cast<const u32x4*>(W + (long)wrow[j] * a.ldw + kb + (s0 + u) * KS + fg * E));
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (s0 + u >= nsl) break;
-      const int k = kb + (s0 + u) * KS + fg * E;
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const int m = i * 16 + fr;
-        u32x4 af = (u32x4){0u, 0u, 0u, 0u};
-        if (m < M) {
-          if constexpr (PRO == PRO_LN) {
-            const float* xr = (const float*)a.x + (long)m * a.ldx + k;
-            const float mu = s_mean[m], rs = s_rstd[m];
-            if constexpr (sizeof(T) == 2) {
-              const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr);
-              const f32x4 x1 = *reinterpret_cast<const f32x4*>(xr + 4);
-              const f32x4 g0 = *reinterpret_cast<const f32x4*>(a.ln_g + k);
-              const f32x4 g1 = *reinterpret_cast<const f32x4*>(a.ln_g + k + 4);
-              const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.ln_b + k);
-              const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.ln_b + k + 4);
-              const f32x4 y0 = (x0 - mu) * rs * g0 + b0;
-              const f32x4 y1 = (x1 - mu) * rs * g1 + b1;
-              af = (u32x4){pack_bf2(y0.x, y0.y), pack_bf2(y0.z, y0.w), pack_bf2(y1.x, y1.y), pack_bf2(y1.z, y1.w)};
-            } else {
-              const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr);
-              const f32x4 g0 = *reinterpret_cast<const f32x4*>(a.ln_g + k);
-              const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.ln_b + k);
-              const f32x4 y0 = (x0 - mu) * rs * g0 + b0;
-              af = (u32x4){__float_as_uint(y0.x), __float_as_uint(y0.y), __float_as_uint(y0.z),
-                           __float_as_uint(y0.w)};
-            }
-          } else {
-            af = *reinterpret_cast<const u32x4*>((const T*)a.x + (long)m * a.ldx + k);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < NTB; ++j) acc[i][j] = mfma_frag(af, wf[u][j], acc[i][j], (T*)nullptr);
-      }
-    }
-  }
-
-  // split-K reduction over the 4 waves
+  const int M = a.M, N = a.N;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -183,15 +91,373 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_kernel(RowsGemmArgs a) {
           bi = n;
         }
       }
+      wave_argmax(bv, bi);
+      if (lane == 0) {
+        a.part_val[(long)m * a.nblk + blockIdx.x] = bv;
+        a.part_idx[(long)m * a.nblk + blockIdx.x] = bi;
+      }
+    }
+  }
+}
+
+
+template <typename T, int MT, int NTB, int PRO, int EPI>
+__global__ __launch_bounds__(256) void vcap_rows_gemm_kernel(RowsGemmArgs a) {
+  constexpr int E = Frag<T>::kElems;
+  constexpr int KS = 4 * E;  // K per MFMA group (32 bf16 / 16 f32)
+  constexpr int U = 4;       // k-slabs of W fragments kept in flight
+  __shared__ float s_mean[MT * 16], s_rstd[MT * 16];
+  __shared__ __attribute__((aligned(16))) float red[4][MT * NTB * 256];
+  __shared__ float lg[EPI == EPI_LOGITS ? MT * 16 : 1][NTB * 16];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int M = a.M, N = a.N, K = a.K;
+  const int n0 = blockIdx.x * NTB * 16;
+
+  if constexpr (PRO == PRO_LN) {
+    const float* X = (const float*)a.x;
+    for (int m = wave; m < M; m += 4) {
+      const float* xr = X + (long)m * a.ldx;
+      float s = 0.f;
+      for (int c = lane; c < K; c += 64) s += xr[c];
+      const float mean = wave_sum(s) / (float)K;
+      float ss = 0.f;
+      for (int c = lane; c < K; c += 64) {
+        const float d = xr[c] - mean;
+        ss += d * d;
+      }
+      const float var = wave_sum(ss) / (float)K;  // whole-wave reduction, outside the lane-0 branch
+      if (lane == 0) {
+        s_mean[m] = mean;
+        s_rstd[m] = rsqrtf(var + a.ln_eps);
+      }
+    }
+    __syncthreads();
+  }
+
+  f32x4 acc[MT][NTB];
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        if (ov > bv || (ov == bv && oi < bi)) {
-          bv = ov;
-          bi = oi;
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const T* W = (const T*)a.w;
+  const int kq = K / 4, kb = wave * kq, nsl = kq / KS;
+  int wrow[NTB];
+#pragma unroll
+  for (int j = 0; j < NTB; ++j) {
+    const int n = n0 + j * 16 + fr;
+    wrow[j] = n < N ? n : N - 1;
+  }
+  for (int s0 = 0; s0 < nsl; s0 += U) {
+    u32x4 wf[U][NTB];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < NTB; ++j)
+        wf[u][j] = __builtin_nontemporal_load(
+            reinterpret_cast<const u32x4*>(W + (long)wrow[j] * a.ldw + kb + min(s0 + u, nsl - 1) * KS + fg * E));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (s0 + u >= nsl) break;
+      const int k = kb + (s0 + u) * KS + fg * E;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int m = min(i * 16 + fr, M - 1);  // rows >= M recompute row M-1 (discarded)
+        u32x4 af = (u32x4){0u, 0u, 0u, 0u};
+        {
+          if constexpr (PRO == PRO_LN) {
+            const float* xr = (const float*)a.x + (long)m * a.ldx + k;
+            const float mu = s_mean[m], rs = s_rstd[m];
+            if constexpr (sizeof(T) == 2) {
+              const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr);
+              const f32x4 x1 = *reinterpret_cast<const f32x4*>(xr + 4);
+              const f32x4 g0 = *reinterpret_cast<const f32x4*>(a.ln_g + k);
+              const f32x4 g1 = *reinterpret_cast<const f32x4*>(a.ln_g + k + 4);
+              const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.ln_b + k);
+              const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.ln_b + k + 4);
+              const f32x4 y0 = (x0 - mu) * rs * g0 + b0;
+              const f32x4 y1 = (x1 - mu) * rs * g1 + b1;
+              af = (u32x4){pack_bf2(y0.x, y0.y), pack_bf2(y0.z, y0.w), pack_bf2(y1.x, y1.y), pack_bf2(y1.z, y1.w)};
+            } else {
+              const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr);
+              const f32x4 g0 = *reinterpret_cast<const f32x4*>(a.ln_g + k);
+              const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.ln_b + k);
+              const f32x4 y0 = (x0 - mu) * rs * g0 + b0;
+              af = (u32x4){__float_as_uint(y0.x), __float_as_uint(y0.y), __float_as_uint(y0.z),
+                           __float_as_uint(y0.w)};
+            }
+          } else {
+            af = *reinterpret_cast<const u32x4*>((const T*)a.x + (long)m * a.ldx + k);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NTB; ++j) acc[i][j] = mfma_frag(af, wf[u][j], acc[i][j], (T*)nullptr);
+      }
+    }
+  }
+
+  rows_epilogue<T, MT, NTB, EPI>(a, acc, red, lg, n0);
+}
+
+// LDS-operand variant for small M (decode).  Everything a workgroup needs from memory is issued
+// up front so the kernel pays ~one memory round trip instead of one per loop iteration:
+//   * the W fragments of the wave's whole K range (8-slab register chunks, nontemporal);
+//   * the epilogue inputs (bias, the residual it will add to, the logits processors' history);
+//   * the activation rows: PRO_DIRECT streams them into LDS by LDS-DMA (global_load_lds_dwordx4),
+//     PRO_LN loads the f32 rows + LayerNorm affine into registers, normalises in-register and
+//     writes the T operand tile.
+// The A tile is unpadded with a 16-byte-chunk XOR swizzle (chunk ^ (row & 15)), so the 16-row
+// ds_read_b128 fragment reads are conflict-free and the DMA image stays lane-linear.
+VCAP_DEV void glds16_dec(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <typename T, int MT, int NTB, int PRO, int EPI>
+__global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  constexpr int E = Frag<T>::kElems;
+  constexpr int KS = 4 * E;
+  constexpr int U = 8;
+  constexpr int MP = MT * 16;
+  constexpr int NE = MT * NTB;  // epilogue elements per thread
+  __shared__ __attribute__((aligned(16))) float red[4][MT * NTB * 256];
+  __shared__ float lg[EPI == EPI_LOGITS ? MP : 1][NTB * 16];
+  __shared__ int s_hist[EPI == EPI_LOGITS ? MP : 1][64];
+  __shared__ int s_ban[EPI == EPI_LOGITS ? MP : 1][64];
+  __shared__ int s_nban[EPI == EPI_LOGITS ? MP : 1];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int M = a.M, N = a.N, K = a.K;
+  const int n0 = blockIdx.x * NTB * 16;
+  const int CPR = K * (int)sizeof(T) / 16;  // 16-byte chunks per A row
+  char* At = dyn;
+
+  // ---- 0) weight fragments
+  const T* W = (const T*)a.w;
+  const int kq = K / 4, kb = wave * kq, nsl = kq / KS;
+  int wrow[NTB];
+#pragma unroll
+  for (int j = 0; j < NTB; ++j) {
+    const int n = n0 + j * 16 + fr;
+    wrow[j] = n < N ? n : N - 1;
+  }
+  u32x4 wa[U][NTB], wb[U][NTB];
+  // Loads are never predicated: a runtime guard around a load makes hipcc wait vmcnt(0) per
+  // load (one HBM round trip each).  Slabs past the wave's range re-read its last slab instead.
+  auto load_chunk = [&](u32x4 (&wf)[U][NTB], int c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int sl = min(c * U + u, nsl - 1);
+#pragma unroll
+      for (int j = 0; j < NTB; ++j)
+        wf[u][j] = __builtin_nontemporal_load(
+            reinterpret_cast<const u32x4*>(W + (long)wrow[j] * a.ldw + kb + sl * KS + fg * E));
+    }
+  };
+  const int nch = (nsl + U - 1) / U;
+  load_chunk(wa, 0);
+  load_chunk(wb, min(1, nch - 1));
+
+  // ---- 1) epilogue inputs
+  float pre_bias[NE], pre_res[NE];
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int e = tid + q * 256;
+    const int tile = e >> 8, within = e & 255;
+    const int m = (tile / NTB) * 16 + (within >> 4), n = n0 + (tile % NTB) * 16 + (within & 15);
+    const int mc = min(m, M - 1), nc = min(n, N - 1);
+    pre_bias[q] = a.bias ? a.bias[nc] : 0.f;
+    pre_res[q] = 0.f;
+    if constexpr (EPI == EPI_RESID) pre_res[q] = ((const float*)a.out)[(long)mc * a.ldo + nc];
+  }
+  if constexpr (EPI == EPI_LOGITS) {
+    for (int i = tid; i < M * 64; i += 256) {
+      const int m = i >> 6, t = i & 63;
+      const int tc = min(t, a.hist_ld - 1);
+      const int h = a.hist[m * a.hist_ld + tc];
+      const int bn = a.banned[m * a.hist_ld + tc];
+      const int nb = a.nbanned[m];
+      s_hist[m][t] = t < a.gen_len ? h : -1;
+      s_ban[m][t] = t < nb ? bn : -1;
+      if (t == 0) s_nban[m] = nb;
+    }
+  }
+
+  // ---- 2) activation rows -> swizzled LDS operand tile
+  if constexpr (PRO == PRO_DIRECT) {
+    const T* X = (const T*)a.x;
+    const int total = MP * CPR / 64;  // 1 KiB wave instructions
+    for (int idx = wave; idx < total; idx += 4) {
+      const int L = idx * 64 + lane;
+      const int row = L / CPR, slot = L % CPR;
+      const int c = slot ^ (row & 15);
+      const int rr = row < M ? row : M - 1;
+      glds16_dec(X + (long)rr * a.ldx + c * E, At + idx * 1024);
+    }
+  } else {
+    constexpr int RPW = MP / 4;         // rows per wave, processed 4 at a time
+    const float* X = (const float*)a.x;
+    f32x4 gv[4], bv[4];
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) {
+      const int c = min(ci * 256 + lane * 4, K - 4);  // clamped, never predicated (see load_chunk)
+      gv[ci] = *reinterpret_cast<const f32x4*>(a.ln_g + c);
+      bv[ci] = *reinterpret_cast<const f32x4*>(a.ln_b + c);
+    }
+#pragma unroll
+    for (int g0 = 0; g0 < RPW; g0 += 4) {
+      f32x4 xv[4][4];
+#pragma unroll
+      for (int ci = 0; ci < 4; ++ci) {
+        const int c = min(ci * 256 + lane * 4, K - 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = min(wave * RPW + g0 + r, M - 1);
+          xv[r][ci] = *reinterpret_cast<const f32x4*>(X + (long)m * a.ldx + c);
         }
       }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wave * RPW + g0 + r;
+        float s = 0.f;
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci)
+          if (ci * 256 + lane * 4 < K) s += (xv[r][ci].x + xv[r][ci].y) + (xv[r][ci].z + xv[r][ci].w);
+        const float mean = wave_sum(s) / (float)K;
+        float ss = 0.f;
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci)
+          if (ci * 256 + lane * 4 < K) {
+            const f32x4 d = xv[r][ci] - mean;
+            ss += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+          }
+        const float rstd = rsqrtf(wave_sum(ss) / (float)K + a.ln_eps);
+        const bool live = m < M;
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci) {
+          const int c = ci * 256 + lane * 4;
+          if (c < K) {
+            const f32x4 y = live ? (xv[r][ci] - mean) * rstd * gv[ci] + bv[ci] : (f32x4){0.f, 0.f, 0.f, 0.f};
+            const int byte = c * (int)sizeof(T);
+            char* dst = At + (long)m * K * sizeof(T) + ((((byte >> 4) ^ (m & 15))) << 4) + (byte & 15);
+            if constexpr (sizeof(T) == 2) {
+              *reinterpret_cast<u32x2*>(dst) = (u32x2){pack_bf2(y.x, y.y), pack_bf2(y.z, y.w)};
+            } else {
+              *reinterpret_cast<f32x4*>(dst) = y;
+            }
+          }
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- 3) MFMA over the wave's K range
+  f32x4 acc[MT][NTB];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto compute_chunk = [&](const u32x4 (&wf)[U][NTB], int c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (c * U + u < nsl) {
+        const int chunk = (kb + (c * U + u) * KS) / E + fg;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const int row = i * 16 + fr;
+          const u32x4 af =
+              *reinterpret_cast<const u32x4*>(At + (long)row * K * sizeof(T) + ((chunk ^ (row & 15)) << 4));
+#pragma unroll
+          for (int j = 0; j < NTB; ++j) acc[i][j] = mfma_frag(af, wf[u][j], acc[i][j], (T*)nullptr);
+        }
+      }
+    }
+  };
+  for (int c = 0; c < nch; c += 2) {
+    compute_chunk(wa, c);
+    if (c + 2 < nch) load_chunk(wa, c + 2);
+    if (c + 1 < nch) {
+      compute_chunk(wb, c + 1);
+      if (c + 3 < nch) load_chunk(wb, c + 3);
+    }
+  }
+
+  // ---- 4) split-K reduction + epilogue
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTB; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][(i * NTB + j) * 256 + (fg * 4 + r) * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int e = tid + q * 256;
+    const int tile = e >> 8, within = e & 255;
+    const int i = tile / NTB, j = tile % NTB;
+    const int row = within >> 4, col = within & 15;
+    const int m = i * 16 + row, n = n0 + j * 16 + col;
+    const bool ok = (m < M) && (n < N);
+    const float v = red[0][e] + red[1][e] + red[2][e] + red[3][e] + pre_bias[q];
+    if constexpr (EPI == EPI_QKV) {
+      if (ok) {
+        const int Ed = N / 3;
+        const int which = n / Ed, within_e = n % Ed;
+        if (which == 0) {
+          ((T*)a.q_out)[(long)m * Ed + within_e] = Num<T>::from_f(v);
+        } else {
+          const int head = within_e >> 6, d = within_e & 63;
+          const int seq = m / a.S_new, pos = a.past + (m % a.S_new);
+          const int page = a.page_table[seq * a.maxp + (pos >> 4)];
+          T* pool = (T*)(which == 1 ? a.kc : a.vc);
+          pool[(((long)page * a.H + head) * 16 + (pos & 15)) * 64 + d] = Num<T>::from_f(v);
+        }
+      }
+    } else if constexpr (EPI == EPI_RESID) {
+      if (ok) ((float*)a.out)[(long)m * a.ldo + n] = pre_res[q] + v;
+    } else if constexpr (EPI == EPI_GELU) {
+      if (ok) ((T*)a.out)[(long)m * a.ldo + n] = Num<T>::from_f(gelu_tanh(v));
+    } else if constexpr (EPI == EPI_STORE) {
+      if (ok) ((T*)a.out)[(long)m * a.ldo + n] = Num<T>::from_f(v);
+    } else {  // EPI_LOGITS
+      if (m < M) {
+        float sv = -INFINITY;
+        if (n < N) {
+          if (a.logits_raw) a.logits_raw[(long)m * N + n] = v;
+          sv = v;
+          if (a.rep_penalty != 1.0f) {
+            bool hit = false;
+            for (int t = 0; t < a.gen_len; ++t) hit |= (s_hist[m][t] == n);
+            if (hit) sv = sv < 0.f ? sv * a.rep_penalty : sv / a.rep_penalty;
+          }
+          for (int t = 0; t < s_nban[m]; ++t)
+            if (s_ban[m][t] == n) sv = -INFINITY;
+          if (n == a.eos && a.gen_len < a.min_new) sv = -INFINITY;
+        }
+        lg[m][j * 16 + col] = sv;
+      }
+    }
+  }
+  if constexpr (EPI == EPI_LOGITS) {
+    __syncthreads();
+    for (int m = wave; m < M; m += 4) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int c = lane; c < NTB * 16; c += 64) {
+        const float v = lg[m][c];
+        const int n = n0 + c;
+        if (v > bv || (v == bv && n < bi)) {
+          bv = v;
+          bi = n;
+        }
+      }
+      wave_argmax(bv, bi);
       if (lane == 0) {
         a.part_val[(long)m * a.nblk + blockIdx.x] = bv;
         a.part_idx[(long)m * a.nblk + blockIdx.x] = bi;
@@ -220,16 +486,19 @@ __global__ __launch_bounds__(256) void vcap_decode_attention_kernel(const T* __r
   s_q[wave][lane] = Num<T>::to_f(q[(long)m * E + h * 64 + lane]);
   __builtin_amdgcn_wave_barrier();
   const int* pt = page_table + seq * maxp;
+  // scores: lane j <-> key j (+64 ...), full 64-dim dot against the broadcast query
   float mx = -INFINITY;
   for (int j = lane; j < ctx; j += 64) {
     const T* krow = kc + (((long)pt[j >> 4] * H + h) * 16 + (j & 15)) * 64;
+    u32x4 kv[64 / Frag<T>::kElems];
+#pragma unroll
+    for (int c = 0; c < 64 / Frag<T>::kElems; ++c) kv[c] = *reinterpret_cast<const u32x4*>(krow + c * Frag<T>::kElems);
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < 64; c += Frag<T>::kElems) {
-      const u32x4 kv = *reinterpret_cast<const u32x4*>(krow + c);
-      const T* ke = reinterpret_cast<const T*>(&kv);
+    for (int c = 0; c < 64 / Frag<T>::kElems; ++c) {
+      const T* ke = reinterpret_cast<const T*>(&kv[c]);
 #pragma unroll
-      for (int e = 0; e < Frag<T>::kElems; ++e) s += s_q[wave][c + e] * Num<T>::to_f(ke[e]);
+      for (int e = 0; e < Frag<T>::kElems; ++e) s += s_q[wave][c * Frag<T>::kElems + e] * Num<T>::to_f(ke[e]);
     }
     s *= 0.125f;
     s_p[wave][j] = s;
@@ -244,12 +513,38 @@ __global__ __launch_bounds__(256) void vcap_decode_attention_kernel(const T* __r
   }
   sum = wave_sum(sum);
   __builtin_amdgcn_wave_barrier();
-  float o = 0.f;
-  for (int j = 0; j < ctx; ++j) {
-    const T* vrow = vc + (((long)pt[j >> 4] * H + h) * 16 + (j & 15)) * 64;
-    o += s_p[wave][j] * Num<T>::to_f(vrow[lane]);
+  // P.V: lane = (key group kg of 4, 4 consecutive dims); partial sums reduced over kg by shuffles
+  const int kg = lane >> 4, d4 = (lane & 15) * 4;
+  f32x4 o = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int jend = (ctx + 3) & ~3;
+#pragma unroll 4
+  for (int j0 = 0; j0 < jend; j0 += 4) {
+    const int jj = j0 + kg;
+    const int j = min(jj, ctx - 1);
+    const T* vrow = vc + (((long)pt[j >> 4] * H + h) * 16 + (j & 15)) * 64 + d4;
+    const float p = jj < ctx ? s_p[wave][j] : 0.f;
+    if constexpr (sizeof(T) == 2) {
+      const u32x2 vv = *reinterpret_cast<const u32x2*>(vrow);
+      o.x += p * bf2f((bf16_t)(vv.x & 0xffff));
+      o.y += p * bf2f((bf16_t)(vv.x >> 16));
+      o.z += p * bf2f((bf16_t)(vv.y & 0xffff));
+      o.w += p * bf2f((bf16_t)(vv.y >> 16));
+    } else {
+      const f32x4 vv = *reinterpret_cast<const f32x4*>(vrow);
+      o += p * vv;
+    }
   }
-  out[(long)m * E + h * 64 + lane] = Num<T>::from_f(o / sum);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = rows_sum(o[e]);
+  if (kg == 0) {
+    const float inv = 1.0f / sum;
+    T* orow = out + (long)m * E + h * 64 + d4;
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<u32x2*>(orow) = (u32x2){pack_bf2(o.x * inv, o.y * inv), pack_bf2(o.z * inv, o.w * inv)};
+    } else {
+      *reinterpret_cast<f32x4*>(orow) = o * inv;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -271,6 +566,36 @@ __global__ __launch_bounds__(256) void vcap_prefill_embed_kernel(const float* __
     float v = (i < P) ? prefix[((long)s * P + i) * E + c] : Num<T>::to_f(wte[(long)prompt.ids[i - P] * E + c]);
     h[(long)m * E + c] = v + wpe[(long)i * E + c];
   }
+}
+
+// Token-id inputs for an externally driven step (beam search / sampling): h[r] = wte[tok[r]] + wpe[pos].
+template <typename T>
+__global__ __launch_bounds__(256) void vcap_embed_tokens_kernel(const int* __restrict__ tok,
+                                                                const T* __restrict__ wte,
+                                                                const float* __restrict__ wpe, float* __restrict__ h,
+                                                                int E, int pos) {
+  const int r = blockIdx.x;
+  const int t = tok[r];
+  for (int c = threadIdx.x; c < E; c += 256) h[(long)r * E + c] = Num<T>::to_f(wte[(long)t * E + c]) + wpe[(long)pos * E + c];
+}
+
+// KV-cache row permutation for beam search: dst row r <- src row src[r], positions [0, len),
+// every layer/head (contiguous [page][H][16][64] pools with identity page tables).
+template <typename T>
+__global__ __launch_bounds__(256) void vcap_kv_gather_kernel(const T* __restrict__ src_pool, T* __restrict__ dst_pool,
+                                                             const int* __restrict__ src_rows, int maxp, int H,
+                                                             int len, long layer_elems, int L) {
+  const int r = blockIdx.x, l = blockIdx.y;
+  const int sr = src_rows[r];
+  const long row_elems = (long)maxp * H * 16 * 64;
+  const T* s = src_pool + l * layer_elems + (long)sr * row_elems;
+  T* d = dst_pool + l * layer_elems + (long)r * row_elems;
+  const int pages = (len + 15) / 16;
+  const long n = (long)pages * H * 16 * 64 / 8;  // 16-byte chunks for bf16 (8 elems) / 2 for f32
+  const int per = 16 / sizeof(T);
+  for (long i = threadIdx.x; i < (long)pages * H * 16 * 64 / per; i += 256)
+    reinterpret_cast<u32x4*>(d)[i] = reinterpret_cast<const u32x4*>(s)[i];
+  (void)n;
 }
 
 // Per-step state init: identity page tables, cleared history / flags.
@@ -345,10 +670,34 @@ __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+constexpr size_t kRowsLdsMax = 120 * 1024;
+
+template <typename T, int MT, int PRO>
+static size_t rows_lds_bytes(const RowsGemmArgs& a) {
+  // the swizzled tile needs whole 256-byte rows; PRO_LN keeps K <= 1024 in registers;
+  // the logits history lives in 64-entry LDS rows
+  if ((a.K * sizeof(T)) % 256 != 0) return ~size_t(0);
+  if (PRO == PRO_LN && a.K > 1024) return ~size_t(0);
+  if (a.hist_ld > 64) return ~size_t(0);
+  return (size_t)MT * 16 * a.K * sizeof(T);
+}
+
 template <typename T, int MT, int NTB, int PRO, int EPI>
 static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
   const int nblk = (a.N + NTB * 16 - 1) / (NTB * 16);
-  hipLaunchKernelGGL((vcap_rows_gemm_kernel<T, MT, NTB, PRO, EPI>), dim3(nblk), dim3(256), 0, s, a);
+  const size_t lds = rows_lds_bytes<T, MT, PRO>(a);
+  if (lds <= kRowsLdsMax) {
+    static bool configured = false;
+    if (!configured) {
+      hipError_t e = hipFuncSetAttribute((const void*)vcap_rows_gemm_lds_kernel<T, MT, NTB, PRO, EPI>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRowsLdsMax);
+      if (e != hipSuccess) return e;
+      configured = true;
+    }
+    hipLaunchKernelGGL((vcap_rows_gemm_lds_kernel<T, MT, NTB, PRO, EPI>), dim3(nblk), dim3(256), lds, s, a);
+  } else {
+    hipLaunchKernelGGL((vcap_rows_gemm_kernel<T, MT, NTB, PRO, EPI>), dim3(nblk), dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 
@@ -428,6 +777,28 @@ hipError_t vcap_prefill_embed_dispatch(int dt, const float* prefix, int P, const
   else
     hipLaunchKernelGGL((vcap_prefill_embed_kernel<float>), dim3(B * S0), dim3(256), 0, s, prefix, P, pr,
                        (const float*)wte, wpe, h, S0, E);
+  return hipGetLastError();
+}
+
+hipError_t vcap_embed_tokens_dispatch(int dt, const int* tok, int rows, const void* wte, const float* wpe, float* h,
+                                      int E, int pos, hipStream_t s) {
+  if (dt == VCAP_DT_BF16)
+    hipLaunchKernelGGL((vcap_embed_tokens_kernel<bf16_t>), dim3(rows), dim3(256), 0, s, tok, (const bf16_t*)wte, wpe, h,
+                       E, pos);
+  else
+    hipLaunchKernelGGL((vcap_embed_tokens_kernel<float>), dim3(rows), dim3(256), 0, s, tok, (const float*)wte, wpe, h, E,
+                       pos);
+  return hipGetLastError();
+}
+
+hipError_t vcap_kv_gather_dispatch(int dt, const void* src_pool, void* dst_pool, const int* src_rows, int rows, int maxp,
+                                   int H, int len, long layer_elems, int L, hipStream_t s) {
+  if (dt == VCAP_DT_BF16)
+    hipLaunchKernelGGL((vcap_kv_gather_kernel<bf16_t>), dim3(rows, L), dim3(256), 0, s, (const bf16_t*)src_pool,
+                       (bf16_t*)dst_pool, src_rows, maxp, H, len, layer_elems, L);
+  else
+    hipLaunchKernelGGL((vcap_kv_gather_kernel<float>), dim3(rows, L), dim3(256), 0, s, (const float*)src_pool,
+                       (float*)dst_pool, src_rows, maxp, H, len, layer_elems, L);
   return hipGetLastError();
 }
 

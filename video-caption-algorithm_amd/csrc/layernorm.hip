@@ -21,12 +21,11 @@ __global__ __launch_bounds__(256) void vcap_layernorm_kernel(const float* __rest
     f32x4 v[MAXV / 4];
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV / 4; ++i) {
-      if (i < nv) {
-        v[i] = *reinterpret_cast<const f32x4*>(xr + i * 256 + lane * 4);
-        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-      }
-    }
+    for (int i = 0; i < MAXV / 4; ++i)  // clamped, unpredicated loads (one round trip)
+      v[i] = *reinterpret_cast<const f32x4*>(xr + min(i, nv - 1) * 256 + lane * 4);
+#pragma unroll
+    for (int i = 0; i < MAXV / 4; ++i)
+      if (i < nv) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     const float mean = wave_sum(s) / (float)D;
     float ss = 0.f;
 #pragma unroll

@@ -182,69 +182,86 @@ int check_gpt2(const vcap_gpt2_desc* d) {
   return 0;
 }
 
+int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_elems, int M, int S_new, int past,
+               hipStream_t s) {
+  const int E = d->n_embd, H = d->n_head, L = d->n_layer;
+  const int dt = d->dtype;
+  const size_t es = esize(dt);
+  for (int l = 0; l < L; ++l) {
+    const vcap_gpt2_layer& ly = d->layers[l];
+    RowsGemmArgs a;
+    memset(&a, 0, sizeof(a));
+    a.M = M;
+    a.ln_eps = d->ln_eps;
+    // 1) ln_1 + c_attn -> q, paged K/V
+    a.x = w.h; a.ldx = E; a.ln_g = ly.ln1_g; a.ln_b = ly.ln1_b;
+    a.w = ly.attn_w; a.ldw = E; a.bias = ly.attn_b; a.N = 3 * E; a.K = E;
+    a.q_out = w.q;
+    a.kc = (char*)w.kc + (size_t)l * page_elems * es;
+    a.vc = (char*)w.vc + (size_t)l * page_elems * es;
+    a.page_table = w.pt; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past;
+    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
+    // 2) causal attention over the paged cache
+    VCAP_TRY(vcap_decode_attention_dispatch(dt, w.q, a.kc, a.vc, w.pt, maxp, w.attn, M, H, S_new, past, s),
+             "decode_attention");
+    // 3) attn c_proj + residual
+    RowsGemmArgs b;
+    memset(&b, 0, sizeof(b));
+    b.M = M; b.x = w.attn; b.ldx = E; b.w = ly.aproj_w; b.ldw = E; b.bias = ly.aproj_b; b.N = E; b.K = E;
+    b.out = w.h; b.ldo = E;
+    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, b, nullptr, s), "attn_c_proj");
+    // 4) ln_2 + c_fc + gelu_new
+    RowsGemmArgs c;
+    memset(&c, 0, sizeof(c));
+    c.M = M; c.x = w.h; c.ldx = E; c.ln_g = ly.ln2_g; c.ln_b = ly.ln2_b; c.ln_eps = d->ln_eps;
+    c.w = ly.fc_w; c.ldw = E; c.bias = ly.fc_b; c.N = 4 * E; c.K = E; c.out = w.act; c.ldo = 4 * E;
+    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_GELU, c, nullptr, s), "c_fc");
+    // 5) mlp c_proj + residual
+    RowsGemmArgs e;
+    memset(&e, 0, sizeof(e));
+    e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.ldw = 4 * E; e.bias = ly.mproj_b; e.N = E;
+    e.K = 4 * E; e.out = w.h; e.ldo = E;
+    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, e, nullptr, s), "mlp_c_proj");
+  }
+  return 0;
+}
+
+// ln_f on each sequence's last row + tied lm_head with the fused processors and argmax partials.
+int run_lm_head(const vcap_gpt2_desc* d, const DecBufs& w, int rows, int S_new, float* logits_raw, int hist_ld,
+                int gen_len, float rep, int min_new, int eos, int* nblk, hipStream_t s) {
+  const int E = d->n_embd;
+  const int dt = d->dtype;
+  VCAP_TRY(vcap_layernorm_dispatch(dt, w.h + (size_t)(S_new - 1) * E, (long)S_new * E, w.xn, E, d->lnf_g, d->lnf_b,
+                                   rows, E, d->ln_eps, s),
+           "ln_f");
+  RowsGemmArgs g;
+  memset(&g, 0, sizeof(g));
+  g.M = rows; g.x = w.xn; g.ldx = E; g.w = d->wte; g.ldw = E; g.bias = nullptr; g.N = d->vocab; g.K = E;
+  g.logits_raw = logits_raw;
+  g.part_val = w.pval; g.part_idx = w.pidx;
+  g.nblk = max_logit_blocks(d->vocab, rows);
+  g.hist = w.hist; g.hist_ld = hist_ld; g.gen_len = gen_len; g.banned = w.banned; g.nbanned = w.nbanned;
+  g.rep_penalty = rep; g.min_new = min_new; g.eos = eos;
+  VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_LOGITS, g, nblk, s), "lm_head");
+  return 0;
+}
+
 int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* ids, int nids,
                  int B, int* out_ids, float* logits_out, const DecBufs& w, int maxp, size_t page_elems,
                  hipStream_t s) {
-  const int E = d->n_embd, H = d->n_head, L = d->n_layer, V = d->vocab;
+  const int E = d->n_embd, V = d->vocab;
   const int P = d->prefix_len, S0 = P + nids, max_new = gp->max_new_tokens;
   const int dt = d->dtype;
-  const size_t es = esize(dt);
   VCAP_TRY(vcap_decode_init_dispatch(w.pt, B, maxp, w.finished, w.nbanned, s), "decode_init");
   VCAP_TRY(vcap_prefill_embed_dispatch(dt, prefix, P, ids, nids, d->wte, d->wpe, w.h, B, E, s), "prefill_embed");
   for (int step = 0; step < max_new; ++step) {
     const int S_new = step == 0 ? S0 : 1;
     const int past = step == 0 ? 0 : S0 + step - 1;
-    const int M = B * S_new;
-    for (int l = 0; l < L; ++l) {
-      const vcap_gpt2_layer& ly = d->layers[l];
-      RowsGemmArgs a;
-      memset(&a, 0, sizeof(a));
-      a.M = M;
-      a.ln_eps = d->ln_eps;
-      // 1) ln_1 + c_attn -> q, paged K/V
-      a.x = w.h; a.ldx = E; a.ln_g = ly.ln1_g; a.ln_b = ly.ln1_b;
-      a.w = ly.attn_w; a.ldw = E; a.bias = ly.attn_b; a.N = 3 * E; a.K = E;
-      a.q_out = w.q;
-      a.kc = (char*)w.kc + (size_t)l * page_elems * es;
-      a.vc = (char*)w.vc + (size_t)l * page_elems * es;
-      a.page_table = w.pt; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past;
-      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
-      // 2) causal attention over the paged cache
-      VCAP_TRY(vcap_decode_attention_dispatch(dt, w.q, a.kc, a.vc, w.pt, maxp, w.attn, M, H, S_new, past, s),
-               "decode_attention");
-      // 3) attn c_proj + residual
-      RowsGemmArgs b;
-      memset(&b, 0, sizeof(b));
-      b.M = M; b.x = w.attn; b.ldx = E; b.w = ly.aproj_w; b.ldw = E; b.bias = ly.aproj_b; b.N = E; b.K = E;
-      b.out = w.h; b.ldo = E;
-      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, b, nullptr, s), "attn_c_proj");
-      // 4) ln_2 + c_fc + gelu_new
-      RowsGemmArgs c;
-      memset(&c, 0, sizeof(c));
-      c.M = M; c.x = w.h; c.ldx = E; c.ln_g = ly.ln2_g; c.ln_b = ly.ln2_b; c.ln_eps = d->ln_eps;
-      c.w = ly.fc_w; c.ldw = E; c.bias = ly.fc_b; c.N = 4 * E; c.K = E; c.out = w.act; c.ldo = 4 * E;
-      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_GELU, c, nullptr, s), "c_fc");
-      // 5) mlp c_proj + residual
-      RowsGemmArgs e;
-      memset(&e, 0, sizeof(e));
-      e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.ldw = 4 * E; e.bias = ly.mproj_b; e.N = E;
-      e.K = 4 * E; e.out = w.h; e.ldo = E;
-      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, e, nullptr, s), "mlp_c_proj");
-    }
-    // ln_f on each sequence's last row, then the tied lm_head with fused processors + argmax partials
-    VCAP_TRY(vcap_layernorm_dispatch(dt, w.h + (size_t)(S_new - 1) * E, (long)S_new * E, w.xn, E, d->lnf_g,
-                                     d->lnf_b, B, E, d->ln_eps, s),
-             "ln_f");
-    RowsGemmArgs g;
-    memset(&g, 0, sizeof(g));
-    g.M = B; g.x = w.xn; g.ldx = E; g.w = d->wte; g.ldw = E; g.bias = nullptr; g.N = V; g.K = E;
-    g.logits_raw = logits_out ? logits_out + (size_t)step * B * V : nullptr;
-    g.part_val = w.pval; g.part_idx = w.pidx;
-    g.nblk = max_logit_blocks(V, B);
-    g.hist = w.hist; g.hist_ld = max_new; g.gen_len = step; g.banned = w.banned; g.nbanned = w.nbanned;
-    g.rep_penalty = gp->repetition_penalty; g.min_new = gp->min_new_tokens; g.eos = gp->eos_token_id;
+    if (int rc = run_layers(d, w, maxp, page_elems, B * S_new, S_new, past, s)) return rc;
     int nblk = 0;
-    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_LOGITS, g, &nblk, s), "lm_head");
+    if (int rc = run_lm_head(d, w, B, S_new, logits_out ? logits_out + (size_t)step * B * V : nullptr, max_new, step,
+                             gp->repetition_penalty, gp->min_new_tokens, gp->eos_token_id, &nblk, s))
+      return rc;
     VCAP_TRY(vcap_decode_finalize_dispatch(dt, w.pval, w.pidx, nblk, B, step, w.finished, w.hist, max_new, w.banned,
                                            w.nbanned, gp->no_repeat_ngram_size, gp->eos_token_id, gp->pad_token_id,
                                            out_ids, max_new, d->wte, d->wpe, w.h, E,
@@ -514,6 +531,86 @@ int vcap_probe_read(const char* site, float* total_ms, int* launches) {
   *launches = p.used;
   p.on = false;
   p.used = 0;
+  return 0;
+}
+
+size_t vcap_gpt2_beam_workspace_bytes(const vcap_gpt2_desc* d, int rows, int S0, int max_new_tokens) {
+  if (check_gpt2(d)) return 0;
+  Carver c(nullptr);
+  int maxp;
+  size_t pe;
+  carve_dec(c, d, rows, S0, max_new_tokens, &maxp, &pe);
+  c.take(pe * d->n_layer * esize(d->dtype));  // reorder scratch (one pool at a time)
+  return c.off;
+}
+
+static int step_setup(const vcap_gpt2_desc* d, int rows, int S0, int max_new, void* ws, size_t ws_bytes, DecBufs* w,
+                      int* maxp, size_t* pe, void** scratch) {
+  if (int rc = check_gpt2(d)) return rc;
+  if (rows <= 0 || rows > 128 || S0 <= 0 || max_new <= 0 || S0 + max_new > d->n_positions)
+    return fail(VCAP_E_ARG, "gpt2 step: bad rows / lengths");
+  if (ws_bytes < vcap_gpt2_beam_workspace_bytes(d, rows, S0, max_new))
+    return fail(VCAP_E_WORKSPACE, "gpt2 step: workspace too small (vcap_gpt2_beam_workspace_bytes)");
+  Carver c(ws);
+  *w = carve_dec(c, d, rows, S0, max_new, maxp, pe);
+  *scratch = c.take(*pe * d->n_layer * esize(d->dtype));
+  return 0;
+}
+
+int vcap_gpt2_prefill(const vcap_gpt2_desc* d, const float* prefix, const int* prompt_ids, int prompt_len, int B,
+                      int rows, int max_new_tokens, float* logits_out, void* workspace, size_t ws_bytes,
+                      void* stream) {
+  const int S0 = d ? d->prefix_len + prompt_len : 0;
+  if (!prefix || !logits_out || B <= 0 || B > rows || prompt_len < 0 || prompt_len > 64 || (prompt_len && !prompt_ids))
+    return fail(VCAP_E_ARG, "vcap_gpt2_prefill: bad arguments");
+  if (B * S0 > 128) return fail(VCAP_E_UNSUPPORTED, "B*(prefix+prompt) must be <= 128 rows");
+  DecBufs w;
+  int maxp;
+  size_t pe;
+  void* scratch;
+  if (int rc = step_setup(d, rows, S0, max_new_tokens, workspace, ws_bytes, &w, &maxp, &pe, &scratch)) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  VCAP_TRY(vcap_decode_init_dispatch(w.pt, rows, maxp, w.finished, w.nbanned, s), "decode_init");
+  VCAP_TRY(vcap_prefill_embed_dispatch(d->dtype, prefix, d->prefix_len, prompt_ids, prompt_len, d->wte, d->wpe, w.h, B,
+                                       d->n_embd, s),
+           "prefill_embed");
+  if (int rc = run_layers(d, w, maxp, pe, B * S0, S0, 0, s)) return rc;
+  int nblk;
+  return run_lm_head(d, w, B, S0, logits_out, 1, 0, 1.0f, 0, -1, &nblk, s);
+}
+
+int vcap_gpt2_step(const vcap_gpt2_desc* d, const int* tokens, int rows, int S0, int max_new_tokens, int pos,
+                   float* logits_out, void* workspace, size_t ws_bytes, void* stream) {
+  if (!tokens || !logits_out || pos < S0 || pos >= S0 + max_new_tokens)
+    return fail(VCAP_E_ARG, "vcap_gpt2_step: bad arguments (S0 <= pos < S0 + max_new_tokens)");
+  DecBufs w;
+  int maxp;
+  size_t pe;
+  void* scratch;
+  if (int rc = step_setup(d, rows, S0, max_new_tokens, workspace, ws_bytes, &w, &maxp, &pe, &scratch)) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  VCAP_TRY(vcap_embed_tokens_dispatch(d->dtype, tokens, rows, d->wte, d->wpe, w.h, d->n_embd, pos, s), "embed_tokens");
+  if (int rc = run_layers(d, w, maxp, pe, rows, 1, pos, s)) return rc;
+  int nblk;
+  return run_lm_head(d, w, rows, 1, logits_out, 1, 0, 1.0f, 0, -1, &nblk, s);
+}
+
+int vcap_gpt2_reorder(const vcap_gpt2_desc* d, const int* src_rows, int rows, int S0, int max_new_tokens, int length,
+                      void* workspace, size_t ws_bytes, void* stream) {
+  if (!src_rows || length <= 0) return fail(VCAP_E_ARG, "vcap_gpt2_reorder: bad arguments");
+  DecBufs w;
+  int maxp;
+  size_t pe;
+  void* scratch;
+  if (int rc = step_setup(d, rows, S0, max_new_tokens, workspace, ws_bytes, &w, &maxp, &pe, &scratch)) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t bytes = pe * d->n_layer * esize(d->dtype);
+  for (void* pool : {w.kc, w.vc}) {
+    VCAP_TRY(vcap_kv_gather_dispatch(d->dtype, pool, scratch, src_rows, rows, maxp, d->n_head, length, (long)pe,
+                                     d->n_layer, s),
+             "kv_gather");
+    VCAP_TRY(hipMemcpyAsync(pool, scratch, bytes, hipMemcpyDeviceToDevice, s), "kv copy-back");
+  }
   return 0;
 }
 

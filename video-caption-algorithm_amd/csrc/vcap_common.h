@@ -44,16 +44,77 @@ VCAP_DEV float gelu_tanh(float x) {
   return 0.5f * x * (1.0f + tanhf(inner));
 }
 
-VCAP_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Cross-lane reductions on the VALU: DPP within 16-lane rows, then the gfx950 permlane16/32
+// swaps across rows.  (__shfl_xor lowers to ds_bpermute, an LDS round trip of ~100+ cycles per
+// step; a 6-step butterfly of those serialises ~700 cycles per reduction.)
+template <int CTRL>
+VCAP_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+VCAP_DEV int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+
+// partner value across 16-lane rows (lane ^ 16) and across wave halves (lane ^ 32)
+VCAP_DEV float xor16_f(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+}
+VCAP_DEV float xor32_f(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+VCAP_DEV int xor16_i(int v) {
+  const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  return (int)((threadIdx.x & 16) ? r[0] : r[1]);
+}
+VCAP_DEV int xor32_i(int v) {
+  const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+  return (int)((threadIdx.x & 32) ? r[0] : r[1]);
 }
 
-VCAP_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+VCAP_DEV float row16_sum(float v) {
+  v += dpp_f<DPP_XOR1>(v);
+  v += dpp_f<DPP_XOR2>(v);
+  v += dpp_f<DPP_HALF_MIRROR>(v);
+  v += dpp_f<DPP_MIRROR>(v);
   return v;
+}
+VCAP_DEV float row16_max(float v) {
+  v = fmaxf(v, dpp_f<DPP_XOR1>(v));
+  v = fmaxf(v, dpp_f<DPP_XOR2>(v));
+  v = fmaxf(v, dpp_f<DPP_HALF_MIRROR>(v));
+  v = fmaxf(v, dpp_f<DPP_MIRROR>(v));
+  return v;
+}
+// sum / max over the 4 lanes {l, l^16, l^32, l^48} (same position in every row)
+VCAP_DEV float rows_sum(float v) {
+  v += xor16_f(v);
+  return v + xor32_f(v);
+}
+VCAP_DEV float rows_max(float v) {
+  v = fmaxf(v, xor16_f(v));
+  return fmaxf(v, xor32_f(v));
+}
+VCAP_DEV float wave_sum(float v) { return rows_sum(row16_sum(v)); }
+VCAP_DEV float wave_max(float v) { return rows_max(row16_max(v)); }
+
+// (value, index) argmax over the wave; ties resolve to the smallest index (torch.argmax order)
+VCAP_DEV void argmax_take(float& bv, int& bi, float ov, int oi) {
+  if (ov > bv || (ov == bv && oi < bi)) {
+    bv = ov;
+    bi = oi;
+  }
+}
+VCAP_DEV void wave_argmax(float& bv, int& bi) {
+  argmax_take(bv, bi, dpp_f<DPP_XOR1>(bv), dpp_i<DPP_XOR1>(bi));
+  argmax_take(bv, bi, dpp_f<DPP_XOR2>(bv), dpp_i<DPP_XOR2>(bi));
+  argmax_take(bv, bi, dpp_f<DPP_HALF_MIRROR>(bv), dpp_i<DPP_HALF_MIRROR>(bi));
+  argmax_take(bv, bi, dpp_f<DPP_MIRROR>(bv), dpp_i<DPP_MIRROR>(bi));
+  argmax_take(bv, bi, xor16_f(bv), xor16_i(bi));
+  argmax_take(bv, bi, xor32_f(bv), xor32_i(bi));
 }
 
 // MFMA wrappers. Both consume one 16-byte fragment per lane per call group:

@@ -71,3 +71,7 @@ hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const in
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,
                                          const float* wpe, float* h, int E, int pos_next, hipStream_t s);
+hipError_t vcap_embed_tokens_dispatch(int dt, const int* tok, int rows, const void* wte, const float* wpe, float* h,
+                                      int E, int pos, hipStream_t s);
+hipError_t vcap_kv_gather_dispatch(int dt, const void* src_pool, void* dst_pool, const int* src_rows, int rows, int maxp,
+                                   int H, int len, long layer_elems, int L, hipStream_t s);

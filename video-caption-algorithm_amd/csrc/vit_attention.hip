@@ -35,16 +35,27 @@ __global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __rest
   T* Vt = reinterpret_cast<T*>(smem + NP * 64 * sizeof(T));
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // ---- stage K (swizzled) and V^T
-  for (int idx = tid; idx < NP * CH; idx += 256) {
+  // ---- stage K (swizzled) and V^T: every load issued before any use (no predicated loads:
+  // a runtime guard around a load makes hipcc wait for each one separately)
+  constexpr int ITERS = NP * CH / 256;
+  static_assert(NP * CH % 256 == 0, "staging loop assumes whole 256-chunk passes");
+  u32x4 kv[ITERS], vv[ITERS];
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int idx = tid + i * 256;
+    const int key = min(idx / CH, N - 1), c = idx % CH;
+    kv[i] = *reinterpret_cast<const u32x4*>(base + (long)key * ld + D + c * E);
+    vv[i] = *reinterpret_cast<const u32x4*>(base + (long)key * ld + 2 * D + c * E);
+  }
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int idx = tid + i * 256;
     const int key = idx / CH, c = idx % CH;
-    u32x4 kv = (u32x4){0u, 0u, 0u, 0u}, vv = (u32x4){0u, 0u, 0u, 0u};
-    if (key < N) {
-      kv = *reinterpret_cast<const u32x4*>(base + (long)key * ld + D + c * E);
-      vv = *reinterpret_cast<const u32x4*>(base + (long)key * ld + 2 * D + c * E);
-    }
-    *reinterpret_cast<u32x4*>(Ks + key * 64 * sizeof(T) + ((c ^ (key & (CH - 1))) << 4)) = kv;
-    const T* ve = reinterpret_cast<const T*>(&vv);
+    const bool live = key < N;
+    const u32x4 z = (u32x4){0u, 0u, 0u, 0u};
+    *reinterpret_cast<u32x4*>(Ks + key * 64 * sizeof(T) + ((c ^ (key & (CH - 1))) << 4)) = live ? kv[i] : z;
+    const u32x4 v = live ? vv[i] : z;
+    const T* ve = reinterpret_cast<const T*>(&v);
 #pragma unroll
     for (int e = 0; e < E; ++e) Vt[(c * E + e) * VS + key] = ve[e];
   }
@@ -83,8 +94,7 @@ __global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __rest
         if (key >= N) st[kt][r] = -INFINITY;
         mx = fmaxf(mx, st[kt][r]);
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = rows_max(mx);
     float sum = 0.f;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
@@ -94,8 +104,7 @@ __global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __rest
         st[kt][r] = p;
         sum += p;
       }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
+    sum = rows_sum(sum);
     const float inv = 1.0f / sum;
 
     // ---- O^T[d][q] = sum_key Vt[d][key] * P^T[key][q]

@@ -76,6 +76,10 @@ SIGNATURES = {
     "vcap_gpt2_generate": (i32, [C.POINTER(GPT2Desc), C.POINTER(GenParams), vp, C.POINTER(C.c_int), i32, i32, vp,
                                  vp, vp, sz, vp]),
     "vcap_graph_cache_clear": (None, []),
+    "vcap_gpt2_beam_workspace_bytes": (sz, [C.POINTER(GPT2Desc), i32, i32, i32]),
+    "vcap_gpt2_prefill": (i32, [C.POINTER(GPT2Desc), vp, C.POINTER(C.c_int), i32, i32, i32, i32, vp, vp, sz, vp]),
+    "vcap_gpt2_step": (i32, [C.POINTER(GPT2Desc), vp, i32, i32, i32, i32, vp, vp, sz, vp]),
+    "vcap_gpt2_reorder": (i32, [C.POINTER(GPT2Desc), vp, i32, i32, i32, i32, vp, sz, vp]),
     "vcap_probe_enable": (i32, [C.c_char_p, i32]),
     "vcap_probe_read": (i32, [C.c_char_p, fp, C.POINTER(C.c_int)]),
 }

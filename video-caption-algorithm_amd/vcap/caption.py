@@ -1,0 +1,162 @@
+"""`VideoCaptionModel`-shaped object on the HIP runtime (the drop-in boundary of SURVEY.md §8b).
+
+Surface kept from the reference (src/models/caption_model.py:11-101, text_decoder.py:12-146):
+  model.encoder(video)            -> [B, 256] f32       (ViTFrameEncoder.forward)
+  model.proj(emb)                 -> emb                (Identity, proj_hidden=0)
+  model.decoder.mapper(emb)       -> [B, P*E] f32       (Linear 256 -> P*E; Dropout is eval-identity)
+  model.decoder.generate(emb, prompt, **kw) -> list[str]   (HF generate semantics, see below)
+  model.decoder.tokenizer / .cond_mode / .prefix_len / .model.config.n_embd / .model.transformer.wte
+  model.generate(video, prompt, **kw)       (VideoCaptionModel.generate: no engine LN-scale)
+plus the batched fast path `generate_ids(video, prompt_ids, ...)` -> int32 [B, max_new] on device.
+
+Decode semantics of decoder.generate (text_decoder.py:131-144): num_beams == 1 and temperature == 1
+-> greedy with RepetitionPenalty, NoRepeatNGram and min_new_tokens (on device, one hipGraph);
+num_beams > 1 -> beam search; num_beams == 1 and temperature != 1 -> sampling (temperature, top-p).
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import configs
+from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, trim_generated
+from .tokenizer import load_tokenizer
+from .weights import normalize_checkpoint, synthetic_state_dict
+
+
+class _Encoder:
+    def __init__(self, hip: HipViTEncoder):
+        self.hip = hip
+
+    def __call__(self, video: torch.Tensor) -> torch.Tensor:
+        emb, _ = self.hip.encode(video, None)
+        return emb
+
+
+class _Identity:
+    def __call__(self, x):
+        return x
+
+
+class _WTE:
+    """decoder.model.transformer.wte: embedding lookup of the packed (device) table."""
+
+    def __init__(self, table: torch.Tensor):
+        self.weight = table
+
+    def __call__(self, ids: torch.Tensor) -> torch.Tensor:
+        return self.weight[ids.to(self.weight.device)].float()
+
+
+class HipTextDecoder:
+    def __init__(self, sd, arch: configs.GPT2Arch, precision: str, device, prefix_len: int = 4,
+                 tokenizer_dir: str = "", use_graph: bool = True):
+        self.arch, self.prefix_len, self.cond_mode = arch, prefix_len, "prefix"
+        self.hip = HipGPT2Decoder(sd, arch, precision, device, prefix_len)
+        self.mapper_op = HipPrefix(sd, arch.n_embd, prefix_len, 0.0, 0.0, device)
+        self.tokenizer = load_tokenizer(tokenizer_dir, arch.eos_token_id)
+        self.use_graph = use_graph
+        self.model = SimpleNamespace(config=SimpleNamespace(n_embd=arch.n_embd, n_layer=arch.n_layer,
+                                                            n_head=arch.n_head, vocab_size=arch.vocab),
+                                     transformer=SimpleNamespace(wte=_WTE(self.hip.wte)))
+
+    def mapper(self, emb: torch.Tensor) -> torch.Tensor:
+        """Linear 256 -> P*E on the HIP path (cupy_linear_mapper / CuPyLinearCompat replacement)."""
+        B = emb.shape[0]
+        return self.mapper_op.project(emb).reshape(B, *emb.shape[1:-1], self.prefix_len * self.arch.n_embd)
+
+    def prefix_embeds(self, emb: torch.Tensor) -> torch.Tensor:
+        return self.mapper_op.project(emb)
+
+    def generate_from_prefix(self, prefix: torch.Tensor, prompt_ids: Sequence[int], *, max_new_tokens: int = 32,
+                             num_beams: int = 1, temperature: float = 1.0, top_p: float = 0.9,
+                             no_repeat_ngram_size: int = 3, repetition_penalty: float = 1.15,
+                             min_new_tokens: int = 8, seed: int = 0) -> List[List[int]]:
+        eos = self.tokenizer.eos_token_id
+        if num_beams == 1 and temperature == 1.0:
+            cfg = GenConfig(max_new_tokens, min_new_tokens, no_repeat_ngram_size, repetition_penalty, eos, eos,
+                            self.use_graph)
+            ids = self.hip.generate_ids(prefix, prompt_ids, cfg)
+            return trim_generated(ids, eos)
+        from . import search
+        if num_beams > 1:
+            return search.beam_search(self.hip, prefix, prompt_ids, num_beams=num_beams,
+                                      max_new_tokens=max_new_tokens, min_new_tokens=min_new_tokens,
+                                      no_repeat_ngram_size=no_repeat_ngram_size,
+                                      repetition_penalty=repetition_penalty, eos=eos)
+        return search.sample(self.hip, prefix, prompt_ids, temperature=temperature, top_p=top_p,
+                             max_new_tokens=max_new_tokens, min_new_tokens=min_new_tokens,
+                             no_repeat_ngram_size=no_repeat_ngram_size, repetition_penalty=repetition_penalty,
+                             eos=eos, seed=seed)
+
+    @torch.no_grad()
+    def generate(self, video_emb: torch.Tensor, prompt: str = "", max_new_tokens: int = 32, num_beams: int = 1,
+                 temperature: float = 1.0, top_p: float = 0.9, no_repeat_ngram_size: int = 3,
+                 repetition_penalty: float = 1.15, min_new_tokens: int = 8) -> List[str]:
+        """GPT2TextDecoder.generate (text_decoder.py:105-146): video_emb [B,256] or [B,1,256]."""
+        prompt_ids = self.tokenizer.encode_prompt(prompt)
+        prefix = self.prefix_embeds(video_emb)
+        rows = self.generate_from_prefix(prefix, prompt_ids, max_new_tokens=max_new_tokens, num_beams=num_beams,
+                                         temperature=temperature, top_p=top_p,
+                                         no_repeat_ngram_size=no_repeat_ngram_size,
+                                         repetition_penalty=repetition_penalty, min_new_tokens=min_new_tokens)
+        return [t.strip() for t in self.tokenizer.batch_decode(rows, skip_special_tokens=True)]
+
+
+class HipVideoCaptionModel:
+    def __init__(self, sd, vit_name: str = "vit_base_patch16_224", gpt2_name: str = "gpt2", prefix_len: int = 4,
+                 precision: str = "bf16", device="cuda", tokenizer_dir: str = "", use_graph: bool = True):
+        self.device = torch.device(device)
+        self.vit_arch, self.gpt2_arch = configs.vit_arch(vit_name), configs.gpt2_arch(gpt2_name)
+        self.hip_encoder = HipViTEncoder(sd, self.vit_arch, precision, self.device)
+        self.encoder = _Encoder(self.hip_encoder)
+        self.proj = _Identity()
+        self.decoder = HipTextDecoder(sd, self.gpt2_arch, precision, self.device, prefix_len, tokenizer_dir,
+                                      use_graph)
+        self._engine_prefix = HipPrefix(sd, self.gpt2_arch.n_embd, prefix_len, 0.6, 0.4, self.device)
+
+    def encode_prefix(self, video: torch.Tensor, ln_scale: Optional[float], in_weight: Optional[float]):
+        """Fused encoder -> proj -> engine LN-scale -> mapper (core/engine.py:43-50 + text_decoder.py:249)."""
+        self._engine_prefix.set_scales(ln_scale if ln_scale and ln_scale > 0 else 0.0,
+                                       in_weight if in_weight and in_weight > 0 else 0.0)
+        return self.hip_encoder.encode(video.to(self.device), self._engine_prefix)
+
+    @torch.no_grad()
+    def generate(self, video: torch.Tensor, prompt: str = "", **gen_kwargs) -> List[str]:
+        """VideoCaptionModel.generate (caption_model.py:93-101): encoder -> proj -> decoder.generate."""
+        emb = self.proj(self.encoder(video.to(self.device)))
+        return self.decoder.generate(emb, prompt=prompt, **gen_kwargs)
+
+    @torch.no_grad()
+    def generate_ids(self, video: torch.Tensor, prompt_ids: Sequence[int], *, ln_scale: float = 0.6,
+                     in_weight: float = 0.4, cfg: Optional[GenConfig] = None) -> torch.Tensor:
+        """Batched fast path: int32 [B, max_new] EOS-padded greedy ids on device."""
+        _, prefix = self.encode_prefix(video, ln_scale, in_weight)
+        eos = self.gpt2_arch.eos_token_id
+        cfg = cfg or GenConfig(24, 8, 3, 1.1, eos, eos, self.decoder.use_graph)
+        return self.decoder.hip.generate_ids(prefix, list(prompt_ids), cfg)
+
+
+def build_state_dict(ckpt: str, vit_name: str, gpt2_name: str, weights_seed: Optional[int], prefix_len: int = 4):
+    """Reference checkpoint (model_loader.py:31-40, 74-75; weights_only load) or seeded random init."""
+    if ckpt:
+        state = torch.load(ckpt, map_location="cpu", weights_only=True)
+        sd = normalize_checkpoint(state)
+        missing = [k for k in synthetic_keys(vit_name, gpt2_name, prefix_len) if k not in sd]
+        if missing:
+            raise KeyError(f"checkpoint {ckpt} lacks {len(missing)} keys, e.g. {missing[:6]}")
+        return sd
+    seed = 1 if weights_seed is None else int(weights_seed)
+    return synthetic_state_dict(seed, configs.vit_arch(vit_name), configs.gpt2_arch(gpt2_name), prefix_len)
+
+
+def synthetic_keys(vit_name: str, gpt2_name: str, prefix_len: int = 4) -> List[str]:
+    va, ga = configs.vit_arch(vit_name), configs.gpt2_arch(gpt2_name)
+    keys = ["encoder.backbone.cls_token", "encoder.backbone.pos_embed", "encoder.backbone.patch_embed.proj.weight",
+            "encoder.proj.weight", "decoder.model.transformer.wte.weight", "decoder.mapper.0.weight"]
+    keys += [f"encoder.backbone.blocks.{i}.attn.qkv.weight" for i in range(va.depth)]
+    keys += [f"decoder.model.transformer.h.{i}.attn.c_attn.weight" for i in range(ga.n_layer)]
+    return keys

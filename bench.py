@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--vit", default="vit_base_patch16_224")
     ap.add_argument("--gpt2", default="gpt2")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--serial", action="store_true",
+                    help="no encode/decode overlap (each step's decode finishes before the next encode starts)")
     ap.add_argument("--cpu-baseline-s", type=float, default=20.0, help="CPU oracle time budget (0 disables)")
     return ap.parse_args()
 
@@ -83,6 +85,8 @@ def main():
     from vcap import configs, prng, weights
     from vcap import _native as N
     from vcap.model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder
+    from vcap.pipeline import CaptionPipeline
+    from vcap.dist import gather_ids
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -106,43 +110,38 @@ def main():
         cfg = GenConfig(args.max_new, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, not args.no_graph)
     else:
         cfg = GenConfig.raw_greedy(args.max_new, ga.eos_token_id, not args.no_graph)
-    ids = torch.empty(B, args.max_new, dtype=torch.int32, device=dev)
-    gathered = torch.empty(world * B, args.max_new, dtype=torch.int32, device=dev) if world > 1 else None
-    stream = torch.cuda.Stream(dev)  # non-default stream: hipGraph replay + the probes' events live here
+    gather = (lambda ids: gather_ids(ids, world)) if world > 1 else None
+    pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev, gather=gather)
 
-    def step(ev=None):
-        e, prefix = enc.encode(video, pre)
-        if ev is not None:
-            ev.record()
-        dec.generate_ids(prefix, [ga.bos_token_id], cfg, out=ids)
-        if gathered is not None:
-            dist.all_gather_into_tensor(gathered, ids)
+    def step(t0=None, t1=None, t2=None):
+        pipe.submit(video, t0, t1, t2)
+        if args.serial:
+            pipe.synchronize()
 
-    with torch.cuda.stream(stream):
-        for _ in range(max(args.warmup, 1)):
-            step()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        lib = N.lib()
-        fc1_launches = va.depth * args.steps
-        N.check(lib.vcap_probe_enable(b"vit.fc1", fc1_launches), "probe")
-        N.check(lib.vcap_probe_enable(b"vit.attention", fc1_launches), "probe")
-        starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-        mids = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-        ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            starts[k].record()
-            step(mids[k])
-            ends[k].record()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
+    for _ in range(max(args.warmup, 1)):
+        step()
+    pipe.synchronize()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    lib = N.lib()
+    fc1_launches = va.depth * args.steps
+    N.check(lib.vcap_probe_enable(b"vit.fc1", fc1_launches), "probe")
+    N.check(lib.vcap_probe_enable(b"vit.attention", fc1_launches), "probe")
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    mids = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(starts[k], mids[k], ends[k])
+    pipe.synchronize()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -177,9 +176,11 @@ def main():
                                    f"{'/[2]' if world > 1 else ''})",
                        "vit": args.vit, "gpt2": args.gpt2, "batch_per_gpu": B, "global_batch": world * B,
                        "frames": T, "max_new_tokens": args.max_new, "decode": args.decode,
-                       "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}"},
-            "p50_latency_ms": p50, "captions_per_s_p50": world * B / (p50 / 1e3),
-            "stage_ms_p50": {"vit_encode_prefix": statistics.median(vit_ms), "gpt2_decode": statistics.median(dec_ms)},
+                       "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}",
+                       "schedule": "serial" if args.serial else "encode(k+1) overlapped with decode(k) on 2 HIP streams"},
+            "p50_latency_ms": p50,
+            "stage_ms_p50": {"vit_encode_prefix": statistics.median(vit_ms),
+                             "prefix_ready_to_ids": statistics.median(dec_ms)},
             "roofline": {"bound": "mfma", "kernel": "vit.fc1 vcap_gemm_kernel<bf16,bf16,1>",
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": None, "flops_per_launch": fc1_flops, "avg_launch_ms": fc1_avg_s * 1e3,

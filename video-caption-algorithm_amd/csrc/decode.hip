@@ -253,9 +253,14 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
     for (int u = 0; u < U; ++u) {
       const int sl = min(c * U + u, nsl - 1);
 #pragma unroll
-      for (int j = 0; j < NTB; ++j)
+      for (int j = 0; j < NTB; ++j) {
+#ifdef VCAP_AB_NO_W  // ablation build: no weight traffic
+        wf[u][j] = (u32x4){(unsigned)(sl + j), 0u, 0u, 0u};
+#else
         wf[u][j] = __builtin_nontemporal_load(
             reinterpret_cast<const u32x4*>(W + (long)wrow[j] * a.ldw + kb + sl * KS + fg * E));
+#endif
+      }
     }
   };
   const int nch = (nsl + U - 1) / U;
@@ -288,7 +293,11 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
   }
 
   // ---- 2) activation rows -> swizzled LDS operand tile
+#ifdef VCAP_AB_NO_A  // ablation build: no activation staging
+  if constexpr (false) {
+#else
   if constexpr (PRO == PRO_DIRECT) {
+#endif
     const T* X = (const T*)a.x;
     const int total = MP * CPR / 64;  // 1 KiB wave instructions
     for (int idx = wave; idx < total; idx += 4) {
@@ -298,7 +307,11 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
       const int rr = row < M ? row : M - 1;
       glds16_dec(X + (long)rr * a.ldx + c * E, At + idx * 1024);
     }
-  } else {
+  } else if constexpr (true
+#ifdef VCAP_AB_NO_A
+                       && false
+#endif
+                       ) {
     constexpr int RPW = MP / 4;         // rows per wave, processed 4 at a time
     const float* X = (const float*)a.x;
     f32x4 gv[4], bv[4];
@@ -405,7 +418,12 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
     const int m = i * 16 + row, n = n0 + j * 16 + col;
     const bool ok = (m < M) && (n < N);
     const float v = red[0][e] + red[1][e] + red[2][e] + red[3][e] + pre_bias[q];
+#ifdef VCAP_AB_NO_EPI  // ablation build: reduction kept, no epilogue work
+    if (v == 1234.5f) ((float*)a.q_out)[tid] = v;
+    if constexpr (false) {
+#else
     if constexpr (EPI == EPI_QKV) {
+#endif
       if (ok) {
         const int Ed = N / 3;
         const int which = n / Ed, within_e = n % Ed;
@@ -614,7 +632,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
     const float* __restrict__ part_val, const int* __restrict__ part_idx, int nblk, int step, int* finished,
     int* hist, int hist_ld, int* banned, int* nbanned, int ngram, int eos, int pad, int* out_ids, int out_ld,
-    const T* __restrict__ wte, const float* __restrict__ wpe, float* __restrict__ h, int E, int pos_next) {
+    const T* __restrict__ wte, const float* __restrict__ wpe, float* __restrict__ h, int E, int pos_next, int vocab) {
   __shared__ float sv[256];
   __shared__ int si[256];
   __shared__ int s_tok;
@@ -645,6 +663,7 @@ __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
   }
   if (tid == 0) {
     int tok = si[0];
+    tok = tok < 0 ? 0 : (tok >= vocab ? vocab - 1 : tok);  // all -inf row (cannot happen with finite logits)
     if (finished[m]) tok = pad;
     out_ids[(long)m * out_ld + step] = tok;
     hist[m * hist_ld + step] = tok;
@@ -812,14 +831,14 @@ hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* fini
 hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const int* part_idx, int nblk, int B,
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,
-                                         const float* wpe, float* h, int E, int pos_next, hipStream_t s) {
+                                         const float* wpe, float* h, int E, int pos_next, int vocab, hipStream_t s) {
   if (dt == VCAP_DT_BF16)
     hipLaunchKernelGGL((vcap_decode_finalize_kernel<bf16_t>), dim3(B), dim3(256), 0, s, part_val, part_idx, nblk,
                        step, finished, hist, hist_ld, banned, nbanned, ngram, eos, pad, out_ids, out_ld,
-                       (const bf16_t*)wte, wpe, h, E, pos_next);
+                       (const bf16_t*)wte, wpe, h, E, pos_next, vocab);
   else
     hipLaunchKernelGGL((vcap_decode_finalize_kernel<float>), dim3(B), dim3(256), 0, s, part_val, part_idx, nblk,
                        step, finished, hist, hist_ld, banned, nbanned, ngram, eos, pad, out_ids, out_ld,
-                       (const float*)wte, wpe, h, E, pos_next);
+                       (const float*)wte, wpe, h, E, pos_next, vocab);
   return hipGetLastError();
 }

@@ -265,7 +265,7 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
     VCAP_TRY(vcap_decode_finalize_dispatch(dt, w.pval, w.pidx, nblk, B, step, w.finished, w.hist, max_new, w.banned,
                                            w.nbanned, gp->no_repeat_ngram_size, gp->eos_token_id, gp->pad_token_id,
                                            out_ids, max_new, d->wte, d->wpe, w.h, E,
-                                           (S0 + step) < d->n_positions ? S0 + step : d->n_positions - 1, s),
+                                           (S0 + step) < d->n_positions ? S0 + step : d->n_positions - 1, V, s),
              "finalize");
   }
   return 0;

@@ -70,7 +70,7 @@ hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* fini
 hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const int* part_idx, int nblk, int B,
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,
-                                         const float* wpe, float* h, int E, int pos_next, hipStream_t s);
+                                         const float* wpe, float* h, int E, int pos_next, int vocab, hipStream_t s);
 hipError_t vcap_embed_tokens_dispatch(int dt, const int* tok, int rows, const void* wte, const float* wpe, float* h,
                                       int E, int pos, hipStream_t s);
 hipError_t vcap_kv_gather_dispatch(int dt, const void* src_pool, void* dst_pool, const int* src_rows, int rows, int maxp,

@@ -19,11 +19,11 @@ ROOT = PKG.parent                      # video-caption-algorithm_amd/
 CSRC = ROOT / "csrc"
 INCLUDE = ROOT.parent / "include"
 LIBDIR = PKG / "_lib"
-LIB = LIBDIR / "libvcap_hip.so"
+LIB = LIBDIR / os.environ.get("VCAP_LIB_NAME", "libvcap_hip.so")
 ARCH = os.environ.get("VCAP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-         "-Wno-unused-result", f"-I{CSRC}", f"-I{INCLUDE}"]
+         "-Wno-unused-result", f"-I{CSRC}", f"-I{INCLUDE}"] + os.environ.get("VCAP_EXTRA_FLAGS", "").split()
 
 
 def sources():
@@ -49,11 +49,11 @@ def _compile(src: Path, obj: Path):
 
 def build(force: bool = False, jobs: int | None = None) -> Path:
     LIBDIR.mkdir(parents=True, exist_ok=True)
-    stamp = LIBDIR / "build.sha256"
+    stamp = LIBDIR / (LIB.name + ".sha256")
     dig = _digest()
     if LIB.exists() and stamp.exists() and stamp.read_text() == dig and not force:
         return LIB
-    objdir = LIBDIR / "obj"
+    objdir = LIBDIR / ("obj" + ("_" + LIB.stem if LIB.name != "libvcap_hip.so" else ""))
     objdir.mkdir(exist_ok=True)
     jobs = jobs or min(8, os.cpu_count() or 1, len(sources()))
     with cf.ThreadPoolExecutor(jobs) as ex:

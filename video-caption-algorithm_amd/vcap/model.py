@@ -109,7 +109,8 @@ class HipViTEncoder:
     def workspace_bytes(self, B: int, T: int) -> int:
         return int(N.lib().vcap_vit_workspace_bytes(C.byref(self.desc), B, T))
 
-    def encode(self, video: torch.Tensor, prefix: Optional["HipPrefix"] = None):
+    def encode(self, video: torch.Tensor, prefix: Optional["HipPrefix"] = None,
+               out_prefix: Optional[torch.Tensor] = None):
         """video [B,T,3,H,W] (or [B,3,H,W]) f32 on device -> (enc_out [B,256] f32, prefix [B,P,E] f32|None)."""
         if video.dim() == 4:
             video = video.unsqueeze(1)
@@ -126,7 +127,13 @@ class HipViTEncoder:
         pre = None
         pd = None
         if prefix is not None:
-            pre = torch.empty(B, prefix.prefix_len, prefix.n_embd, dtype=torch.float32, device=video.device)
+            shape = (B, prefix.prefix_len, prefix.n_embd)
+            if out_prefix is not None:
+                if tuple(out_prefix.shape) != shape or out_prefix.dtype != torch.float32 or not out_prefix.is_contiguous():
+                    raise ValueError(f"out_prefix must be contiguous f32 {shape}")
+                pre = out_prefix
+            else:
+                pre = torch.empty(*shape, dtype=torch.float32, device=video.device)
             pd = C.byref(prefix.desc)
         nbytes = self.workspace_bytes(B, T)
         ws = self.ws.get(nbytes)

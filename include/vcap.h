@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 1
+#define VCAP_ABI_VERSION 2
 
 enum { VCAP_DT_F32 = 0, VCAP_DT_BF16 = 1 };
 enum { VCAP_E_ARG = -1000, VCAP_E_WORKSPACE = -1001, VCAP_E_UNSUPPORTED = -1002 };
@@ -74,20 +74,24 @@ typedef struct vcap_prefix_desc {
   const float* mapper_b;
 } vcap_prefix_desc;
 
+/* GPT-2 projection weights are passed ROWS-PACKED: the torch Linear-layout [N, K] matrix
+ * (Conv1D weights transposed) rearranged by vcap_rows_pack() into MFMA-fragment order, so each
+ * decode weight load is one contiguous 1 KiB wave instruction (layout in csrc/decode.hip). */
 typedef struct vcap_gpt2_layer {
   const float* ln1_g; const float* ln1_b;
-  const void* attn_w; const float* attn_b;   /* [3E, E] (Conv1D transposed) */
-  const void* aproj_w; const float* aproj_b; /* [E, E] */
+  const void* attn_w; const float* attn_b;   /* packed [3E, E] (c_attn Conv1D transposed) */
+  const void* aproj_w; const float* aproj_b; /* packed [E, E] */
   const float* ln2_g; const float* ln2_b;
-  const void* fc_w; const float* fc_b;       /* [4E, E] */
-  const void* mproj_w; const float* mproj_b; /* [E, 4E] */
+  const void* fc_w; const float* fc_b;       /* packed [4E, E] */
+  const void* mproj_w; const float* mproj_b; /* packed [E, 4E] */
 } vcap_gpt2_layer;
 
 typedef struct vcap_gpt2_desc {
   int dtype;
   int n_embd, n_layer, n_head, vocab, n_positions, prefix_len;
   float ln_eps;              /* 1e-5 */
-  const void* wte;           /* [vocab, E] (also the tied lm_head) */
+  const void* wte;           /* [vocab, E] token embedding (plain layout, row gathers) */
+  const void* lm_head;       /* packed [vocab, E]: the tied lm_head = vcap_rows_pack(wte) */
   const float* wpe;          /* [n_positions, E] f32 */
   const float* lnf_g; const float* lnf_b;
   const vcap_gpt2_layer* layers; /* host array of n_layer entries */
@@ -118,6 +122,13 @@ int vcap_vit_pool_temporal(int dtype, const void* feat, void* out, int bsz, int 
                            int pool_gap, void* stream);
 int vcap_prefix_project(const float* emb, int B, int video_dim, const vcap_prefix_desc* pd, float* prefix_out,
                         void* stream);
+
+/* ---- weight layout for the GPT-2 decoder (one-time, at model load) ----
+ * vcap_rows_packed_bytes: bytes of the packed copy of a [N, K] matrix (N rounded up to 16).
+ * vcap_rows_pack: w [N, K] row stride ldw (elements, 16-byte aligned rows) -> packed.
+ * K must be a multiple of 32 (bf16) / 16 (f32); the decoder needs n_embd % 128 == 0. */
+size_t vcap_rows_packed_bytes(int dtype, int N, int K);
+int vcap_rows_pack(int dtype, const void* w, int64_t ldw, int N, int K, void* packed, void* stream);
 
 /* ---- fused paths ---- */
 size_t vcap_vit_workspace_bytes(const vcap_vit_desc* d, int B, int T);

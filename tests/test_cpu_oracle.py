@@ -115,6 +115,10 @@ def test_workspace_queries_without_gpu():
     gd = N.GPT2Desc(dtype=N.DT_BF16, n_embd=768, n_layer=12, n_head=12, vocab=50257, n_positions=1024, prefix_len=4,
                     ln_eps=1e-5, layers=gl)
     assert N.lib().vcap_gpt2_workspace_bytes(C.byref(gd), 8, 5, 24) > 0
+    # rows-packed decoder weights: whole 16-row tiles x K/KS slabs x 1 KiB (csrc/decode.hip)
+    assert N.lib().vcap_rows_packed_bytes(N.DT_BF16, 50257, 768) == 3142 * 24 * 1024
+    assert N.lib().vcap_rows_packed_bytes(N.DT_F32, 2304, 768) == 144 * 48 * 1024
+    assert N.lib().vcap_rows_packed_bytes(N.DT_BF16, 16, 100) == 0
     bad = N.VitDesc(dtype=N.DT_BF16, dim=100, depth=1, heads=1, patch=16, image=224, mlp=400, video_dim=256,
                     kpad=768, ln_eps=1e-6, layers=layers)
     assert N.lib().vcap_vit_workspace_bytes(C.byref(bad), 1, 1) == 0

@@ -7,335 +7,349 @@
 //   then logits = ln_f(h) . wte^T, RepetitionPenalty -> NoRepeatNGram -> MinNewTokens -> argmax.
 //
 // Rows: M = B*S_new rows per step (S_new = prefix+prompt length at prefill, 1 while decoding).
-// Weights are pre-transposed to [N, K] (K contiguous) so every projection is a skinny MFMA
-// GEMM: a workgroup of 4 waves owns NTB 16-column tiles for all M rows and splits K over its
-// waves (4 independent HBM streams per workgroup); partial tiles are summed through LDS.
-// LayerNorm is fused into the A-operand prologue (each workgroup recomputes the M row
-// statistics from the L2-resident residual stream instead of paying a launch + round trip).
+// Every projection is a skinny MFMA GEMM: a workgroup of 4 waves owns NTB 16-column tiles for
+// all M rows and splits K over its waves; partial tiles are summed through LDS.  LayerNorm is
+// fused into the A-operand prologue (each workgroup recomputes the M row statistics from the
+// L2-resident residual stream instead of paying a launch + round trip).
+//
+// Weights are stored "rows-packed" (vcap_rows_pack): for n-tile t (16 output features) and K
+// slab g (one MFMA K step: 32 bf16 / 16 f32), the 64 lanes' B fragments are 1 KiB contiguous,
+//   packed[(t * (K/KS) + g) * 64 + lane] (16 B) = W[16t + (lane & 15)][KS*g + E*(lane >> 4) ...+E)
+// so every weight load is one fully coalesced 1 KiB wave instruction and a wave's whole K range
+// of a tile is one contiguous run (rows >= N are zero).
 #include "vcap_common.h"
 #include "vcap_kernels.h"
 
-// Split-K reduction over the 4 waves through LDS + the role's epilogue.
-template <typename T, int MT, int NTB, int EPI>
-VCAP_DEV void rows_epilogue(const RowsGemmArgs& a, f32x4 (&acc)[MT][NTB], float (*red)[MT * NTB * 256],
-                            float (*lg)[NTB * 16], int n0) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int M = a.M, N = a.N;
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NTB; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[wave][(i * NTB + j) * 256 + (fg * 4 + r) * 16 + fr] = acc[i][j][r];
-  __syncthreads();
+#include <algorithm>
 
-  for (int e = tid; e < MT * NTB * 256; e += 256) {
-    const int tile = e >> 8, within = e & 255;
-    const int i = tile / NTB, j = tile % NTB;
-    const int row = within >> 4, col = within & 15;
-    const int m = i * 16 + row, n = n0 + j * 16 + col;
-    float v = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+// ------------------------------------------------------------------------------------------------
+// Weight packing (one-time, at model load).
+template <typename T>
+__global__ __launch_bounds__(256) void vcap_rows_pack_kernel(const T* __restrict__ w, long ldw, int N, int K,
+                                                             u32x4* __restrict__ packed) {
+  constexpr int E = Frag<T>::kElems, KS = 4 * E;
+  const int nslab = K / KS;
+  const long total = (long)((N + 15) / 16) * nslab * 64;
+  for (long c = blockIdx.x * 256L + threadIdx.x; c < total; c += (long)gridDim.x * 256L) {
+    const int lane = (int)(c & 63);
+    const long tg = c >> 6;
+    const int g = (int)(tg % nslab);
+    const long row = (tg / nslab) * 16 + (lane & 15);
+    u32x4 v = (u32x4){0u, 0u, 0u, 0u};
+    if (row < N) v = *reinterpret_cast<const u32x4*>(w + row * ldw + g * KS + (lane >> 4) * E);
+    packed[c] = v;
+  }
+}
+
+VCAP_DEV const u32x4* packed_frag(const void* w, int tile, int nslab, int slab, int lane) {
+  return reinterpret_cast<const u32x4*>(w) + ((long)tile * nslab + slab) * 64 + lane;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Shared epilogue of the rows kernels: split-K partial tiles (red[wave]) -> role output.
+// pre_bias/pre_res were loaded at kernel start; s_rep/s_ban flag the processors' tokens that fall
+// in this workgroup's column range.
+template <typename T, int MT, int NTB, int EPI>
+VCAP_DEV void rows_epilogue(const RowsGemmArgs& a, int m0, const float (*red)[MT * NTB * 256], const float* pre_bias,
+                            const float* pre_res, float (*lg)[NTB * 16], const unsigned char (*s_rep)[NTB * 16],
+                            const unsigned char (*s_ban)[NTB * 16], int n0) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = a.M, N = a.N;
+  const int row = tid >> 4, col = tid & 15;
+#pragma unroll
+  for (int q = 0; q < MT * NTB; ++q) {
+    const int e = tid + q * 256;
+    const int i = q / NTB, j = q % NTB;
+    const int ml = i * 16 + row, m = m0 + ml, n = n0 + j * 16 + col;
     const bool ok = (m < M) && (n < N);
-    if (ok && a.bias) v += a.bias[n];
+    const float v = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]) + pre_bias[q];
     if constexpr (EPI == EPI_QKV) {
       if (ok) {
         const int Ed = N / 3;
-        const int which = n / Ed, within_e = n % Ed;
+        const int which = n / Ed, within_e = n - which * Ed;
         if (which == 0) {
           ((T*)a.q_out)[(long)m * Ed + within_e] = Num<T>::from_f(v);
         } else {
           const int head = within_e >> 6, d = within_e & 63;
-          const int seq = m / a.S_new, pos = a.past + (m % a.S_new);
+          const int seq = m / a.S_new, pos = a.past + (m - seq * a.S_new);
           const int page = a.page_table[seq * a.maxp + (pos >> 4)];
           T* pool = (T*)(which == 1 ? a.kc : a.vc);
           pool[(((long)page * a.H + head) * 16 + (pos & 15)) * 64 + d] = Num<T>::from_f(v);
         }
       }
     } else if constexpr (EPI == EPI_RESID) {
-      if (ok) ((float*)a.out)[(long)m * a.ldo + n] += v;
+      if (ok) ((float*)a.out)[(long)m * a.ldo + n] = pre_res[q] + v;
     } else if constexpr (EPI == EPI_GELU) {
       if (ok) ((T*)a.out)[(long)m * a.ldo + n] = Num<T>::from_f(gelu_tanh(v));
     } else if constexpr (EPI == EPI_STORE) {
       if (ok) ((T*)a.out)[(long)m * a.ldo + n] = Num<T>::from_f(v);
-    } else {  // EPI_LOGITS
+    } else {  // EPI_LOGITS: RepetitionPenalty -> NoRepeatNGram -> MinNewTokens (HF processor order)
       if (m < M) {
         float sv = -INFINITY;
         if (n < N) {
           if (a.logits_raw) a.logits_raw[(long)m * N + n] = v;
           sv = v;
-          if (a.rep_penalty != 1.0f) {
-            bool hit = false;
-            for (int t = 0; t < a.gen_len; ++t) hit |= (a.hist[m * a.hist_ld + t] == n);
-            if (hit) sv = sv < 0.f ? sv * a.rep_penalty : sv / a.rep_penalty;
-          }
-          const int nb = a.nbanned ? a.nbanned[m] : 0;
-          for (int t = 0; t < nb; ++t)
-            if (a.banned[m * a.hist_ld + t] == n) sv = -INFINITY;
+          if (s_rep[ml][j * 16 + col]) sv = sv < 0.f ? sv * a.rep_penalty : sv / a.rep_penalty;
+          if (s_ban[ml][j * 16 + col]) sv = -INFINITY;
           if (n == a.eos && a.gen_len < a.min_new) sv = -INFINITY;
         }
-        lg[m][j * 16 + col] = sv;
+        lg[ml][j * 16 + col] = sv;
       }
     }
   }
   if constexpr (EPI == EPI_LOGITS) {
     __syncthreads();
-    for (int m = wave; m < M; m += 4) {
+    for (int ml = wave; ml < MT * 16 && m0 + ml < M; ml += 4) {
       float bv = -INFINITY;
       int bi = 0x7fffffff;
-      for (int c = lane; c < NTB * 16; c += 64) {
-        const float v = lg[m][c];
-        const int n = n0 + c;
-        if (v > bv || (v == bv && n < bi)) {
-          bv = v;
-          bi = n;
-        }
-      }
+      for (int c = lane; c < NTB * 16; c += 64) argmax_take(bv, bi, lg[ml][c], n0 + c);
       wave_argmax(bv, bi);
       if (lane == 0) {
-        a.part_val[(long)m * a.nblk + blockIdx.x] = bv;
-        a.part_idx[(long)m * a.nblk + blockIdx.x] = bi;
+        a.part_val[(long)(m0 + ml) * a.nblk + blockIdx.x] = bv;
+        a.part_idx[(long)(m0 + ml) * a.nblk + blockIdx.x] = bi;
       }
     }
   }
 }
 
+// Processor token flags for the logits epilogue: zero (kernel start), then mark after the loads.
+template <int MP, int NTB>
+VCAP_DEV void proc_flags_zero(unsigned char (*s_rep)[NTB * 16], unsigned char (*s_ban)[NTB * 16]) {
+  for (int i = threadIdx.x; i < MP * NTB * 16; i += 256) {
+    (&s_rep[0][0])[i] = 0;
+    (&s_ban[0][0])[i] = 0;
+  }
+}
 
-template <typename T, int MT, int NTB, int PRO, int EPI>
-__global__ __launch_bounds__(256) void vcap_rows_gemm_kernel(RowsGemmArgs a) {
-  constexpr int E = Frag<T>::kElems;
-  constexpr int KS = 4 * E;  // K per MFMA group (32 bf16 / 16 f32)
-  constexpr int U = 4;       // k-slabs of W fragments kept in flight
-  __shared__ float s_mean[MT * 16], s_rstd[MT * 16];
-  __shared__ __attribute__((aligned(16))) float red[4][MT * NTB * 256];
-  __shared__ float lg[EPI == EPI_LOGITS ? MT * 16 : 1][NTB * 16];
+// History / ban-list tokens of the (m, t) pairs this thread owns (t < 64), loaded early.
+template <int MT>
+struct ProcToks {
+  int h[MT * 4], b[MT * 4], nb[MT * 4];
+  VCAP_DEV void load(const RowsGemmArgs& a, int m0) {
+#pragma unroll
+    for (int q = 0; q < MT * 4; ++q) {
+      const int i = threadIdx.x + q * 256;
+      const int m = min(m0 + (i >> 6), a.M - 1), t = min(i & 63, a.hist_ld - 1);
+      h[q] = a.hist[m * a.hist_ld + t];
+      b[q] = a.banned[m * a.hist_ld + t];
+      nb[q] = a.nbanned[m];
+    }
+  }
+  template <int NTB>
+  VCAP_DEV void mark(const RowsGemmArgs& a, int m0, int n0, unsigned char (*s_rep)[NTB * 16],
+                     unsigned char (*s_ban)[NTB * 16]) const {
+#pragma unroll
+    for (int q = 0; q < MT * 4; ++q) {
+      const int i = threadIdx.x + q * 256;
+      const int m = i >> 6, t = i & 63;  // m: row within the chunk
+      if (m0 + m >= a.M) continue;
+      const unsigned hc = (unsigned)(h[q] - n0), bc = (unsigned)(b[q] - n0);
+      if (a.rep_penalty != 1.0f && t < a.gen_len && hc < (unsigned)(NTB * 16)) s_rep[m][hc] = 1;
+      if (t < nb[q] && bc < (unsigned)(NTB * 16)) s_ban[m][bc] = 1;
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// Decode GEMV (M <= 32 rows): everything a workgroup needs from memory is issued at kernel start,
+// in the order it is consumed (vmcnt retires in issue order):
+//   1. the activation operand - PRO_DIRECT: MFMA A fragments straight to VGPRs; PRO_LN: the f32
+//      rows + LayerNorm affine (normalised in registers, written once to an XOR-swizzled LDS tile);
+//   2. the wave's whole K range of rows-packed weights: NSL slabs x NTB tiles of 1 KiB loads,
+//      nontemporal (each weight byte is read by exactly one CU per step);
+//   3. the epilogue inputs (bias, residual, processors' token lists).
+// NSL (slabs per wave = K / (4*KS)) is a template parameter, so the loads are fully unrolled with
+// no clamped duplicates and the compiler counts vmcnt exactly.
+template <typename T, int MT, int NTB, int PRO, int EPI, int NSL>
+__global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char dyn[];  // PRO_LN: A tile [MT*16][K] T
+  constexpr int E = Frag<T>::kElems, KS = 4 * E, MP = MT * 16, NE = MT * NTB;
+  constexpr int LGM = EPI == EPI_LOGITS ? MP : 1;
+  constexpr int KC = NSL * KS * 4 / 256;  // f32x4 chunks per lane of a K-long row (PRO_LN)
+  constexpr int RPW = MP / 4;             // LN rows per wave
+  __shared__ __attribute__((aligned(16))) float red[4][NE * 256];
+  __shared__ float lg[LGM][NTB * 16];
+  __shared__ unsigned char s_rep[LGM][NTB * 16], s_ban[LGM][NTB * 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int M = a.M, N = a.N, K = a.K;
+  const int m0 = blockIdx.y * MP;
   const int n0 = blockIdx.x * NTB * 16;
+  const int nslab = 4 * NSL;  // = K / KS
+  const int g0 = wave * NSL;
+  const int ntiles = (N + 15) >> 4;
 
-  if constexpr (PRO == PRO_LN) {
+  if constexpr (EPI == EPI_LOGITS) proc_flags_zero<MP, NTB>(s_rep, s_ban);
+
+  // ---- 1) activation operand
+  u32x4 af[PRO == PRO_DIRECT ? MT : 1][PRO == PRO_DIRECT ? NSL : 1];
+  f32x4 xv[PRO == PRO_LN ? RPW : 1][KC > 0 ? KC : 1], gv[KC > 0 ? KC : 1], bv[KC > 0 ? KC : 1];
+  if constexpr (PRO == PRO_DIRECT) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const T* xr = (const T*)a.x + (long)min(m0 + i * 16 + fr, M - 1) * a.ldx + fg * E;
+#pragma unroll
+      for (int s = 0; s < NSL; ++s) af[i][s] = *reinterpret_cast<const u32x4*>(xr + (g0 + s) * KS);
+    }
+  } else {
     const float* X = (const float*)a.x;
-    for (int m = wave; m < M; m += 4) {
-      const float* xr = X + (long)m * a.ldx;
-      float s = 0.f;
-      for (int c = lane; c < K; c += 64) s += xr[c];
-      const float mean = wave_sum(s) / (float)K;
-      float ss = 0.f;
-      for (int c = lane; c < K; c += 64) {
-        const float d = xr[c] - mean;
-        ss += d * d;
-      }
-      const float var = wave_sum(ss) / (float)K;  // whole-wave reduction, outside the lane-0 branch
-      if (lane == 0) {
-        s_mean[m] = mean;
-        s_rstd[m] = rsqrtf(var + a.ln_eps);
-      }
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const float* xr = X + (long)min(m0 + wave + 4 * r, M - 1) * a.ldx + lane * 4;
+#pragma unroll
+      for (int c = 0; c < KC; ++c) xv[r][c] = *reinterpret_cast<const f32x4*>(xr + c * 256);
     }
-    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      gv[c] = *reinterpret_cast<const f32x4*>(a.ln_g + c * 256 + lane * 4);
+      bv[c] = *reinterpret_cast<const f32x4*>(a.ln_b + c * 256 + lane * 4);
+    }
   }
 
-  f32x4 acc[MT][NTB];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NTB; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const T* W = (const T*)a.w;
-  const int kq = K / 4, kb = wave * kq, nsl = kq / KS;
-  int wrow[NTB];
+  // ---- 2) weights
+  u32x4 wf[NSL][NTB];
 #pragma unroll
   for (int j = 0; j < NTB; ++j) {
-    const int n = n0 + j * 16 + fr;
-    wrow[j] = n < N ? n : N - 1;
-  }
-  for (int s0 = 0; s0 < nsl; s0 += U) {
-    u32x4 wf[U][NTB];
+    const u32x4* wp = packed_frag(a.w, min(n0 / 16 + j, ntiles - 1), nslab, g0, lane);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int j = 0; j < NTB; ++j)
-        wf[u][j] = __builtin_nontemporal_load(
-            reinterpret_cast<const u32x4*>(W + (long)wrow[j] * a.ldw + kb + min(s0 + u, nsl - 1) * KS + fg * E));
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (s0 + u >= nsl) break;
-      const int k = kb + (s0 + u) * KS + fg * E;
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const int m = min(i * 16 + fr, M - 1);  // rows >= M recompute row M-1 (discarded)
-        u32x4 af = (u32x4){0u, 0u, 0u, 0u};
-        {
-          if constexpr (PRO == PRO_LN) {
-            const float* xr = (const float*)a.x + (long)m * a.ldx + k;
-            const float mu = s_mean[m], rs = s_rstd[m];
-            if constexpr (sizeof(T) == 2) {
-              const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr);
-              const f32x4 x1 = *reinterpret_cast<const f32x4*>(xr + 4);
-              const f32x4 g0 = *reinterpret_cast<const f32x4*>(a.ln_g + k);
-              const f32x4 g1 = *reinterpret_cast<const f32x4*>(a.ln_g + k + 4);
-              const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.ln_b + k);
-              const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.ln_b + k + 4);
-              const f32x4 y0 = (x0 - mu) * rs * g0 + b0;
-              const f32x4 y1 = (x1 - mu) * rs * g1 + b1;
-              af = (u32x4){pack_bf2(y0.x, y0.y), pack_bf2(y0.z, y0.w), pack_bf2(y1.x, y1.y), pack_bf2(y1.z, y1.w)};
-            } else {
-              const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr);
-              const f32x4 g0 = *reinterpret_cast<const f32x4*>(a.ln_g + k);
-              const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.ln_b + k);
-              const f32x4 y0 = (x0 - mu) * rs * g0 + b0;
-              af = (u32x4){__float_as_uint(y0.x), __float_as_uint(y0.y), __float_as_uint(y0.z),
-                           __float_as_uint(y0.w)};
-            }
-          } else {
-            af = *reinterpret_cast<const u32x4*>((const T*)a.x + (long)m * a.ldx + k);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < NTB; ++j) acc[i][j] = mfma_frag(af, wf[u][j], acc[i][j], (T*)nullptr);
-      }
-    }
+    for (int s = 0; s < NSL; ++s) wf[s][j] = __builtin_nontemporal_load(wp + s * 64);
   }
 
-  rows_epilogue<T, MT, NTB, EPI>(a, acc, red, lg, n0);
-}
-
-// LDS-operand variant for small M (decode).  Everything a workgroup needs from memory is issued
-// up front so the kernel pays ~one memory round trip instead of one per loop iteration:
-//   * the W fragments of the wave's whole K range (8-slab register chunks, nontemporal);
-//   * the epilogue inputs (bias, the residual it will add to, the logits processors' history);
-//   * the activation rows: PRO_DIRECT streams them into LDS by LDS-DMA (global_load_lds_dwordx4),
-//     PRO_LN loads the f32 rows + LayerNorm affine into registers, normalises in-register and
-//     writes the T operand tile.
-// The A tile is unpadded with a 16-byte-chunk XOR swizzle (chunk ^ (row & 15)), so the 16-row
-// ds_read_b128 fragment reads are conflict-free and the DMA image stays lane-linear.
-VCAP_DEV void glds16_dec(const void* g, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-
-template <typename T, int MT, int NTB, int PRO, int EPI>
-__global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char dyn[];
-  constexpr int E = Frag<T>::kElems;
-  constexpr int KS = 4 * E;
-  constexpr int U = 8;
-  constexpr int MP = MT * 16;
-  constexpr int NE = MT * NTB;  // epilogue elements per thread
-  __shared__ __attribute__((aligned(16))) float red[4][MT * NTB * 256];
-  __shared__ float lg[EPI == EPI_LOGITS ? MP : 1][NTB * 16];
-  __shared__ int s_hist[EPI == EPI_LOGITS ? MP : 1][64];
-  __shared__ int s_ban[EPI == EPI_LOGITS ? MP : 1][64];
-  __shared__ int s_nban[EPI == EPI_LOGITS ? MP : 1];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int M = a.M, N = a.N, K = a.K;
-  const int n0 = blockIdx.x * NTB * 16;
-  const int CPR = K * (int)sizeof(T) / 16;  // 16-byte chunks per A row
-  char* At = dyn;
-
-  // ---- 0) weight fragments
-  const T* W = (const T*)a.w;
-  const int kq = K / 4, kb = wave * kq, nsl = kq / KS;
-  int wrow[NTB];
-#pragma unroll
-  for (int j = 0; j < NTB; ++j) {
-    const int n = n0 + j * 16 + fr;
-    wrow[j] = n < N ? n : N - 1;
-  }
-  u32x4 wa[U][NTB], wb[U][NTB];
-  // Loads are never predicated: a runtime guard around a load makes hipcc wait vmcnt(0) per
-  // load (one HBM round trip each).  Slabs past the wave's range re-read its last slab instead.
-  auto load_chunk = [&](u32x4 (&wf)[U][NTB], int c) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int sl = min(c * U + u, nsl - 1);
-#pragma unroll
-      for (int j = 0; j < NTB; ++j) {
-#ifdef VCAP_AB_NO_W  // ablation build: no weight traffic
-        wf[u][j] = (u32x4){(unsigned)(sl + j), 0u, 0u, 0u};
-#else
-        wf[u][j] = __builtin_nontemporal_load(
-            reinterpret_cast<const u32x4*>(W + (long)wrow[j] * a.ldw + kb + sl * KS + fg * E));
-#endif
-      }
-    }
-  };
-  const int nch = (nsl + U - 1) / U;
-  load_chunk(wa, 0);
-  load_chunk(wb, min(1, nch - 1));
-
-  // ---- 1) epilogue inputs
+  // ---- 3) epilogue inputs
   float pre_bias[NE], pre_res[NE];
 #pragma unroll
   for (int q = 0; q < NE; ++q) {
-    const int e = tid + q * 256;
-    const int tile = e >> 8, within = e & 255;
-    const int m = (tile / NTB) * 16 + (within >> 4), n = n0 + (tile % NTB) * 16 + (within & 15);
+    const int m = m0 + (q / NTB) * 16 + (tid >> 4), n = n0 + (q % NTB) * 16 + (tid & 15);
     const int mc = min(m, M - 1), nc = min(n, N - 1);
     pre_bias[q] = a.bias ? a.bias[nc] : 0.f;
     pre_res[q] = 0.f;
     if constexpr (EPI == EPI_RESID) pre_res[q] = ((const float*)a.out)[(long)mc * a.ldo + nc];
   }
-  if constexpr (EPI == EPI_LOGITS) {
-    for (int i = tid; i < M * 64; i += 256) {
-      const int m = i >> 6, t = i & 63;
-      const int tc = min(t, a.hist_ld - 1);
-      const int h = a.hist[m * a.hist_ld + tc];
-      const int bn = a.banned[m * a.hist_ld + tc];
-      const int nb = a.nbanned[m];
-      s_hist[m][t] = t < a.gen_len ? h : -1;
-      s_ban[m][t] = t < nb ? bn : -1;
-      if (t == 0) s_nban[m] = nb;
+  ProcToks<EPI == EPI_LOGITS ? MT : 1> toks;
+  if constexpr (EPI == EPI_LOGITS) toks.load(a, m0);
+
+  // ---- LayerNorm in registers -> swizzled LDS tile (waits only for step 1's loads)
+  if constexpr (PRO == PRO_LN) {
+    const int rowb = K * (int)sizeof(T);
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int m = wave + 4 * r;  // row within the chunk
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < KC; ++c) s += (xv[r][c].x + xv[r][c].y) + (xv[r][c].z + xv[r][c].w);
+      const float mean = wave_sum(s) / (float)K;
+      float ss = 0.f;
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        const f32x4 d = xv[r][c] - mean;
+        ss += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+      }
+      const float rstd = rsqrtf(wave_sum(ss) / (float)K + a.ln_eps);
+      const bool live = m0 + m < M;
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        const f32x4 y = live ? (xv[r][c] - mean) * rstd * gv[c] + bv[c] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        const int byte = (c * 256 + lane * 4) * (int)sizeof(T);
+        char* dst = dyn + (long)m * rowb + ((((byte >> 4) ^ (m & 15))) << 4) + (byte & 15);
+        if constexpr (sizeof(T) == 2) {
+          *reinterpret_cast<u32x2*>(dst) = (u32x2){pack_bf2(y.x, y.y), pack_bf2(y.z, y.w)};
+        } else {
+          *reinterpret_cast<f32x4*>(dst) = y;
+        }
+      }
+    }
+  }
+  if constexpr (PRO == PRO_LN || EPI == EPI_LOGITS) __syncthreads();
+
+  // ---- MFMA over the wave's K range
+  f32x4 acc[MT][NTB];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NSL; ++s) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      u32x4 A;
+      if constexpr (PRO == PRO_DIRECT) {
+        A = af[i][s];
+      } else {
+        const int row = i * 16 + fr, chunk = (g0 + s) * 4 + fg;
+        A = *reinterpret_cast<const u32x4*>(dyn + (long)row * K * sizeof(T) + ((chunk ^ (row & 15)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) acc[i][j] = mfma_frag(A, wf[s][j], acc[i][j], (T*)nullptr);
     }
   }
 
-  // ---- 2) activation rows -> swizzled LDS operand tile
-#ifdef VCAP_AB_NO_A  // ablation build: no activation staging
-  if constexpr (false) {
-#else
-  if constexpr (PRO == PRO_DIRECT) {
-#endif
-    const T* X = (const T*)a.x;
-    const int total = MP * CPR / 64;  // 1 KiB wave instructions
-    for (int idx = wave; idx < total; idx += 4) {
-      const int L = idx * 64 + lane;
-      const int row = L / CPR, slot = L % CPR;
-      const int c = slot ^ (row & 15);
-      const int rr = row < M ? row : M - 1;
-      glds16_dec(X + (long)rr * a.ldx + c * E, At + idx * 1024);
-    }
-  } else if constexpr (true
-#ifdef VCAP_AB_NO_A
-                       && false
-#endif
-                       ) {
-    constexpr int RPW = MP / 4;         // rows per wave, processed 4 at a time
+  // ---- split-K reduction + epilogue
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTB; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][(i * NTB + j) * 256 + (fg * 4 + r) * 16 + fr] = acc[i][j][r];
+  if constexpr (EPI == EPI_LOGITS) toks.template mark<NTB>(a, m0, n0, s_rep, s_ban);
+  __syncthreads();
+  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0);
+}
+
+// ------------------------------------------------------------------------------------------------
+// General rows kernel (prefill rows, f32 parity mode, shapes outside the GEMV instantiations):
+// rows [m0, m0 + MT*16) of a blockIdx.y row chunk; weights streamed in double-buffered chunks of
+// U slabs; PRO_DIRECT A fragments ride along with each weight chunk in registers, PRO_LN rows
+// are normalised into a swizzled LDS tile first (K <= 1024).
+template <typename T, int MT, int NTB, int PRO, int EPI>
+__global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  constexpr int E = Frag<T>::kElems;
+  constexpr int KS = 4 * E;
+  constexpr int U = NTB >= 4 ? 2 : 8 / NTB;  // slabs per chunk: U*NTB weight fragments in flight
+  constexpr int MP = MT * 16;
+  constexpr int NE = MT * NTB;
+  constexpr int LGM = EPI == EPI_LOGITS ? MP : 1;
+  __shared__ __attribute__((aligned(16))) float red[4][NE * 256];
+  __shared__ float lg[LGM][NTB * 16];
+  __shared__ unsigned char s_rep[LGM][NTB * 16], s_ban[LGM][NTB * 16];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int m0 = blockIdx.y * MP;
+  const int M = a.M, N = a.N, K = a.K;
+  const int n0 = blockIdx.x * NTB * 16;
+  const int nslab = K / KS, nsl = nslab / 4, g0 = wave * nsl;
+  const int ntiles = (N + 15) >> 4;
+  const int rowb = K * (int)sizeof(T);
+  if constexpr (EPI == EPI_LOGITS) proc_flags_zero<MP, NTB>(s_rep, s_ban);
+
+  // ---- PRO_LN: rows -> LayerNorm -> swizzled LDS tile
+  if constexpr (PRO == PRO_LN) {
+    constexpr int RPW = MP / 4;
     const float* X = (const float*)a.x;
     f32x4 gv[4], bv[4];
 #pragma unroll
     for (int ci = 0; ci < 4; ++ci) {
-      const int c = min(ci * 256 + lane * 4, K - 4);  // clamped, never predicated (see load_chunk)
+      const int c = min(ci * 256 + lane * 4, K - 4);  // clamped, never predicated
       gv[ci] = *reinterpret_cast<const f32x4*>(a.ln_g + c);
       bv[ci] = *reinterpret_cast<const f32x4*>(a.ln_b + c);
     }
 #pragma unroll
-    for (int g0 = 0; g0 < RPW; g0 += 4) {
+    for (int gq = 0; gq < RPW; gq += 4) {
       f32x4 xv[4][4];
 #pragma unroll
       for (int ci = 0; ci < 4; ++ci) {
         const int c = min(ci * 256 + lane * 4, K - 4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = min(wave * RPW + g0 + r, M - 1);
+          const int m = min(m0 + wave + 4 * (gq + r), M - 1);
           xv[r][ci] = *reinterpret_cast<const f32x4*>(X + (long)m * a.ldx + c);
         }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = wave * RPW + g0 + r;
+        const int ml = wave + 4 * (gq + r);
         float s = 0.f;
 #pragma unroll
         for (int ci = 0; ci < 4; ++ci)
@@ -349,14 +363,14 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
             ss += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
           }
         const float rstd = rsqrtf(wave_sum(ss) / (float)K + a.ln_eps);
-        const bool live = m < M;
+        const bool live = m0 + ml < M;
 #pragma unroll
         for (int ci = 0; ci < 4; ++ci) {
           const int c = ci * 256 + lane * 4;
           if (c < K) {
             const f32x4 y = live ? (xv[r][ci] - mean) * rstd * gv[ci] + bv[ci] : (f32x4){0.f, 0.f, 0.f, 0.f};
             const int byte = c * (int)sizeof(T);
-            char* dst = At + (long)m * K * sizeof(T) + ((((byte >> 4) ^ (m & 15))) << 4) + (byte & 15);
+            char* dst = dyn + (long)ml * rowb + ((((byte >> 4) ^ (ml & 15))) << 4) + (byte & 15);
             if constexpr (sizeof(T) == 2) {
               *reinterpret_cast<u32x2*>(dst) = (u32x2){pack_bf2(y.x, y.y), pack_bf2(y.z, y.w)};
             } else {
@@ -367,160 +381,135 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 
-  // ---- 3) MFMA over the wave's K range
+  // ---- weight (+ PRO_DIRECT activation) fragments, chunk by chunk.  Loads are never predicated
+  // (a guarded load waits vmcnt(0) on its own); slabs past the wave's range re-read its last slab.
+  u32x4 wa[U][NTB], wb[U][NTB], xa[PRO == PRO_DIRECT ? U : 1][MT], xb[PRO == PRO_DIRECT ? U : 1][MT];
+  auto load_chunk = [&](u32x4 (&wf)[U][NTB], u32x4 (&xf)[PRO == PRO_DIRECT ? U : 1][MT], int c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int sl = min(c * U + u, nsl - 1);
+      if constexpr (PRO == PRO_DIRECT) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          xf[u][i] = *reinterpret_cast<const u32x4*>((const T*)a.x + (long)min(m0 + i * 16 + fr, M - 1) * a.ldx +
+                                                     (g0 + sl) * KS + fg * E);
+      }
+#pragma unroll
+      for (int j = 0; j < NTB; ++j)
+        wf[u][j] = __builtin_nontemporal_load(
+            packed_frag(a.w, min(n0 / 16 + j, ntiles - 1), nslab, g0 + sl, lane));
+    }
+  };
+  const int nch = (nsl + U - 1) / U;
+  load_chunk(wa, xa, 0);
+  if (nch > 1) load_chunk(wb, xb, 1);
+
+  // ---- epilogue inputs
+  float pre_bias[NE], pre_res[NE];
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int m = m0 + (q / NTB) * 16 + (tid >> 4), n = n0 + (q % NTB) * 16 + (tid & 15);
+    const int mc = min(m, M - 1), nc = min(n, N - 1);
+    pre_bias[q] = a.bias ? a.bias[nc] : 0.f;
+    pre_res[q] = 0.f;
+    if constexpr (EPI == EPI_RESID) pre_res[q] = ((const float*)a.out)[(long)mc * a.ldo + nc];
+  }
+  ProcToks<EPI == EPI_LOGITS ? MT : 1> toks;
+  if constexpr (EPI == EPI_LOGITS) toks.load(a, m0);
+  if constexpr (PRO == PRO_LN || EPI == EPI_LOGITS) __syncthreads();
+
+  // ---- MFMA over the wave's K range
   f32x4 acc[MT][NTB];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NTB; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  auto compute_chunk = [&](const u32x4 (&wf)[U][NTB], int c) {
+  auto compute_chunk = [&](const u32x4 (&wf)[U][NTB], const u32x4 (&xf)[PRO == PRO_DIRECT ? U : 1][MT], int c) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (c * U + u < nsl) {
-        const int chunk = (kb + (c * U + u) * KS) / E + fg;
+        const int chunk = (g0 + c * U + u) * 4 + fg;
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
-          const int row = i * 16 + fr;
-          const u32x4 af =
-              *reinterpret_cast<const u32x4*>(At + (long)row * K * sizeof(T) + ((chunk ^ (row & 15)) << 4));
+          u32x4 A;
+          if constexpr (PRO == PRO_DIRECT) {
+            A = xf[u][i];
+          } else {
+            const int row = i * 16 + fr;
+            A = *reinterpret_cast<const u32x4*>(dyn + (long)row * rowb + ((chunk ^ (row & 15)) << 4));
+          }
 #pragma unroll
-          for (int j = 0; j < NTB; ++j) acc[i][j] = mfma_frag(af, wf[u][j], acc[i][j], (T*)nullptr);
+          for (int j = 0; j < NTB; ++j) acc[i][j] = mfma_frag(A, wf[u][j], acc[i][j], (T*)nullptr);
         }
       }
     }
   };
   for (int c = 0; c < nch; c += 2) {
-    compute_chunk(wa, c);
-    if (c + 2 < nch) load_chunk(wa, c + 2);
+    compute_chunk(wa, xa, c);
+    if (c + 2 < nch) load_chunk(wa, xa, c + 2);
     if (c + 1 < nch) {
-      compute_chunk(wb, c + 1);
-      if (c + 3 < nch) load_chunk(wb, c + 3);
+      compute_chunk(wb, xb, c + 1);
+      if (c + 3 < nch) load_chunk(wb, xb, c + 3);
     }
   }
 
-  // ---- 4) split-K reduction + epilogue
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NTB; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wave][(i * NTB + j) * 256 + (fg * 4 + r) * 16 + fr] = acc[i][j][r];
+  if constexpr (EPI == EPI_LOGITS) toks.template mark<NTB>(a, m0, n0, s_rep, s_ban);
   __syncthreads();
-#pragma unroll
-  for (int q = 0; q < NE; ++q) {
-    const int e = tid + q * 256;
-    const int tile = e >> 8, within = e & 255;
-    const int i = tile / NTB, j = tile % NTB;
-    const int row = within >> 4, col = within & 15;
-    const int m = i * 16 + row, n = n0 + j * 16 + col;
-    const bool ok = (m < M) && (n < N);
-    const float v = red[0][e] + red[1][e] + red[2][e] + red[3][e] + pre_bias[q];
-#ifdef VCAP_AB_NO_EPI  // ablation build: reduction kept, no epilogue work
-    if (v == 1234.5f) ((float*)a.q_out)[tid] = v;
-    if constexpr (false) {
-#else
-    if constexpr (EPI == EPI_QKV) {
-#endif
-      if (ok) {
-        const int Ed = N / 3;
-        const int which = n / Ed, within_e = n % Ed;
-        if (which == 0) {
-          ((T*)a.q_out)[(long)m * Ed + within_e] = Num<T>::from_f(v);
-        } else {
-          const int head = within_e >> 6, d = within_e & 63;
-          const int seq = m / a.S_new, pos = a.past + (m % a.S_new);
-          const int page = a.page_table[seq * a.maxp + (pos >> 4)];
-          T* pool = (T*)(which == 1 ? a.kc : a.vc);
-          pool[(((long)page * a.H + head) * 16 + (pos & 15)) * 64 + d] = Num<T>::from_f(v);
-        }
-      }
-    } else if constexpr (EPI == EPI_RESID) {
-      if (ok) ((float*)a.out)[(long)m * a.ldo + n] = pre_res[q] + v;
-    } else if constexpr (EPI == EPI_GELU) {
-      if (ok) ((T*)a.out)[(long)m * a.ldo + n] = Num<T>::from_f(gelu_tanh(v));
-    } else if constexpr (EPI == EPI_STORE) {
-      if (ok) ((T*)a.out)[(long)m * a.ldo + n] = Num<T>::from_f(v);
-    } else {  // EPI_LOGITS
-      if (m < M) {
-        float sv = -INFINITY;
-        if (n < N) {
-          if (a.logits_raw) a.logits_raw[(long)m * N + n] = v;
-          sv = v;
-          if (a.rep_penalty != 1.0f) {
-            bool hit = false;
-            for (int t = 0; t < a.gen_len; ++t) hit |= (s_hist[m][t] == n);
-            if (hit) sv = sv < 0.f ? sv * a.rep_penalty : sv / a.rep_penalty;
-          }
-          for (int t = 0; t < s_nban[m]; ++t)
-            if (s_ban[m][t] == n) sv = -INFINITY;
-          if (n == a.eos && a.gen_len < a.min_new) sv = -INFINITY;
-        }
-        lg[m][j * 16 + col] = sv;
-      }
-    }
-  }
-  if constexpr (EPI == EPI_LOGITS) {
-    __syncthreads();
-    for (int m = wave; m < M; m += 4) {
-      float bv = -INFINITY;
-      int bi = 0x7fffffff;
-      for (int c = lane; c < NTB * 16; c += 64) {
-        const float v = lg[m][c];
-        const int n = n0 + c;
-        if (v > bv || (v == bv && n < bi)) {
-          bv = v;
-          bi = n;
-        }
-      }
-      wave_argmax(bv, bi);
-      if (lane == 0) {
-        a.part_val[(long)m * a.nblk + blockIdx.x] = bv;
-        a.part_idx[(long)m * a.nblk + blockIdx.x] = bi;
-      }
-    }
-  }
+  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0);
 }
 
 // ------------------------------------------------------------------------------------------------
 // Causal attention of S_new query rows per sequence over the paged cache (positions 0..past+i).
+// One wave per (row, head).  The sequence's page ids are read once (lane p holds page p) and
+// broadcast with ds_bpermute, so no K/V load waits on a dependent page-table load.
+// Scores: lane j <-> key j (+64 ...), full 64-dim dot.  P.V: lane = (key group kg of 8, 8
+// consecutive dims d8), partial sums reduced over the 8 key groups by DPP + permlane swaps.
 template <typename T>
 __global__ __launch_bounds__(256) void vcap_decode_attention_kernel(const T* __restrict__ q, const T* __restrict__ kc,
                                                                     const T* __restrict__ vc,
                                                                     const int* __restrict__ page_table, int maxp,
                                                                     T* __restrict__ out, int M, int H, int S_new,
                                                                     int past) {
+  constexpr int E8 = Frag<T>::kElems;  // elements per 16-byte chunk
   __shared__ float s_q[4][64];
   __shared__ float s_p[4][1024];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int item = blockIdx.x * 4 + wave;
   if (item >= M * H) return;
-  const int m = item / H, h = item % H;
+  const int m = item / H, h = item - m * H;
   const int E = H * 64;
-  const int seq = m / S_new, qpos = past + (m % S_new);
+  const int seq = m / S_new, qpos = past + (m - seq * S_new);
   const int ctx = qpos + 1;
+  const int my_page = page_table[seq * maxp + min(lane, maxp - 1)];
   s_q[wave][lane] = Num<T>::to_f(q[(long)m * E + h * 64 + lane]);
   __builtin_amdgcn_wave_barrier();
-  const int* pt = page_table + seq * maxp;
-  // scores: lane j <-> key j (+64 ...), full 64-dim dot against the broadcast query
   float mx = -INFINITY;
-  for (int j = lane; j < ctx; j += 64) {
-    const T* krow = kc + (((long)pt[j >> 4] * H + h) * 16 + (j & 15)) * 64;
-    u32x4 kv[64 / Frag<T>::kElems];
+  for (int j0 = 0; j0 < ctx; j0 += 64) {
+    const int j = min(j0 + lane, ctx - 1);
+    const int page = __shfl(my_page, j >> 4);
+    const T* krow = kc + (((long)page * H + h) * 16 + (j & 15)) * 64;
+    u32x4 kv[64 / E8];
 #pragma unroll
-    for (int c = 0; c < 64 / Frag<T>::kElems; ++c) kv[c] = *reinterpret_cast<const u32x4*>(krow + c * Frag<T>::kElems);
+    for (int c = 0; c < 64 / E8; ++c) kv[c] = *reinterpret_cast<const u32x4*>(krow + c * E8);
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < 64 / Frag<T>::kElems; ++c) {
+    for (int c = 0; c < 64 / E8; ++c) {
       const T* ke = reinterpret_cast<const T*>(&kv[c]);
 #pragma unroll
-      for (int e = 0; e < Frag<T>::kElems; ++e) s += s_q[wave][c * Frag<T>::kElems + e] * Num<T>::to_f(ke[e]);
+      for (int e = 0; e < E8; ++e) s += s_q[wave][c * E8 + e] * Num<T>::to_f(ke[e]);
     }
     s *= 0.125f;
-    s_p[wave][j] = s;
-    mx = fmaxf(mx, s);
+    if (j0 + lane < ctx) {
+      s_p[wave][j0 + lane] = s;
+      mx = fmaxf(mx, s);
+    }
   }
   mx = wave_max(mx);
   float sum = 0.f;
@@ -531,36 +520,48 @@ __global__ __launch_bounds__(256) void vcap_decode_attention_kernel(const T* __r
   }
   sum = wave_sum(sum);
   __builtin_amdgcn_wave_barrier();
-  // P.V: lane = (key group kg of 4, 4 consecutive dims); partial sums reduced over kg by shuffles
-  const int kg = lane >> 4, d4 = (lane & 15) * 4;
-  f32x4 o = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int jend = (ctx + 3) & ~3;
+  const int kg = lane >> 3, d8 = (lane & 7) * 8;
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = 0.f;
 #pragma unroll 4
-  for (int j0 = 0; j0 < jend; j0 += 4) {
+  for (int j0 = 0; j0 < ctx; j0 += 8) {
     const int jj = j0 + kg;
     const int j = min(jj, ctx - 1);
-    const T* vrow = vc + (((long)pt[j >> 4] * H + h) * 16 + (j & 15)) * 64 + d4;
+    const int page = __shfl(my_page, j >> 4);
+    const T* vrow = vc + (((long)page * H + h) * 16 + (j & 15)) * 64 + d8;
     const float p = jj < ctx ? s_p[wave][j] : 0.f;
     if constexpr (sizeof(T) == 2) {
-      const u32x2 vv = *reinterpret_cast<const u32x2*>(vrow);
-      o.x += p * bf2f((bf16_t)(vv.x & 0xffff));
-      o.y += p * bf2f((bf16_t)(vv.x >> 16));
-      o.z += p * bf2f((bf16_t)(vv.y & 0xffff));
-      o.w += p * bf2f((bf16_t)(vv.y >> 16));
+      const u32x4 vv = *reinterpret_cast<const u32x4*>(vrow);
+      const unsigned w4[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[2 * e] += p * bf2f((bf16_t)(w4[e] & 0xffff));
+        o[2 * e + 1] += p * bf2f((bf16_t)(w4[e] >> 16));
+      }
     } else {
-      const f32x4 vv = *reinterpret_cast<const f32x4*>(vrow);
-      o += p * vv;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(vrow);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(vrow + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] += p * v0[e];
+        o[4 + e] += p * v1[e];
+      }
     }
   }
+  // reduce over the 8 key groups: lane ^ 8 (row_ror:8 inside a 16-lane row), then ^16, ^32
 #pragma unroll
-  for (int e = 0; e < 4; ++e) o[e] = rows_sum(o[e]);
+  for (int e = 0; e < 8; ++e) o[e] = rows_sum(o[e] + dpp_f<0x128>(o[e]));
   if (kg == 0) {
     const float inv = 1.0f / sum;
-    T* orow = out + (long)m * E + h * 64 + d4;
+    T* orow = out + (long)m * E + h * 64 + d8;
     if constexpr (sizeof(T) == 2) {
-      *reinterpret_cast<u32x2*>(orow) = (u32x2){pack_bf2(o.x * inv, o.y * inv), pack_bf2(o.z * inv, o.w * inv)};
+      *reinterpret_cast<u32x4*>(orow) =
+          (u32x4){pack_bf2(o[0] * inv, o[1] * inv), pack_bf2(o[2] * inv, o[3] * inv),
+                  pack_bf2(o[4] * inv, o[5] * inv), pack_bf2(o[6] * inv, o[7] * inv)};
     } else {
-      *reinterpret_cast<f32x4*>(orow) = o * inv;
+      *reinterpret_cast<f32x4*>(orow) = (f32x4){o[0], o[1], o[2], o[3]} * inv;
+      *reinterpret_cast<f32x4*>(orow + 4) = (f32x4){o[4], o[5], o[6], o[7]} * inv;
     }
   }
 }
@@ -627,152 +628,186 @@ __global__ void vcap_decode_init_kernel(int* page_table, int B, int maxp, int* f
 }
 
 // Reduce the per-workgroup argmax partials, apply EOS padding, record the token, precompute the
-// n-gram ban list for the next step and write the next input embedding wte[tok] + wpe[pos].
+// n-gram ban list for the next step (one thread per n-gram start, history staged in LDS) and
+// write the next input embedding wte[tok] + wpe[pos].
 template <typename T>
 __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
     const float* __restrict__ part_val, const int* __restrict__ part_idx, int nblk, int step, int* finished,
     int* hist, int hist_ld, int* banned, int* nbanned, int ngram, int eos, int pad, int* out_ids, int out_ld,
     const T* __restrict__ wte, const float* __restrict__ wpe, float* __restrict__ h, int E, int pos_next, int vocab) {
-  __shared__ float sv[256];
-  __shared__ int si[256];
-  __shared__ int s_tok;
-  const int m = blockIdx.x, tid = threadIdx.x;
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  __shared__ int s_h[1024];
+  __shared__ int s_tok, s_nb;
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int t = tid; t < step; t += 256) s_h[t] = hist[m * hist_ld + t];
   float bv = -INFINITY;
   int bi = 0x7fffffff;
-  for (int b = tid; b < nblk; b += 256) {
-    const float v = part_val[(long)m * nblk + b];
-    const int i = part_idx[(long)m * nblk + b];
-    if (v > bv || (v == bv && i < bi)) {
-      bv = v;
-      bi = i;
-    }
+  for (int b = tid; b < nblk; b += 256) argmax_take(bv, bi, part_val[(long)m * nblk + b], part_idx[(long)m * nblk + b]);
+  wave_argmax(bv, bi);
+  if (lane == 0) {
+    sv[wave] = bv;
+    si[wave] = bi;
   }
-  sv[tid] = bv;
-  si[tid] = bi;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) {
-      const float ov = sv[tid + o];
-      const int oi = si[tid + o];
-      if (ov > sv[tid] || (ov == sv[tid] && oi < si[tid])) {
-        sv[tid] = ov;
-        si[tid] = oi;
-      }
-    }
-    __syncthreads();
-  }
   if (tid == 0) {
-    int tok = si[0];
+    for (int w = 1; w < 4; ++w) argmax_take(bv, bi, sv[w], si[w]);
+    int tok = bi;
     tok = tok < 0 ? 0 : (tok >= vocab ? vocab - 1 : tok);  // all -inf row (cannot happen with finite logits)
     if (finished[m]) tok = pad;
     out_ids[(long)m * out_ld + step] = tok;
     hist[m * hist_ld + step] = tok;
+    s_h[step] = tok;
     if (tok == eos) finished[m] = 1;
-    // NoRepeatNGram ban list for the next step over the L = step+1 generated tokens
-    const int L = step + 1;
-    int nb = 0;
-    if (ngram > 0 && L + 1 >= ngram) {
-      const int* hs = hist + m * hist_ld;
-      for (int i = 0; i + ngram <= L; ++i) {
-        bool match = true;
-        for (int t = 0; t < ngram - 1; ++t) match &= (hs[i + t] == hs[L - ngram + 1 + t]);
-        if (match) banned[m * hist_ld + nb++] = hs[i + ngram - 1];
-      }
-    }
-    nbanned[m] = nb;
     s_tok = tok;
+    s_nb = 0;
   }
   __syncthreads();
+  // NoRepeatNGram ban list for the next step over the L = step+1 generated tokens
+  const int L = step + 1;
+  if (ngram > 0 && L + 1 >= ngram) {
+    for (int i = tid; i + ngram <= L; i += 256) {
+      bool match = true;
+      for (int t = 0; t < ngram - 1; ++t) match &= (s_h[i + t] == s_h[L - ngram + 1 + t]);
+      if (match) banned[m * hist_ld + atomicAdd(&s_nb, 1)] = s_h[i + ngram - 1];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) nbanned[m] = s_nb;
   const int tok = s_tok;
   for (int c = tid; c < E; c += 256)
     h[(long)m * E + c] = Num<T>::to_f(wte[(long)tok * E + c]) + wpe[(long)pos_next * E + c];
 }
 
 // ------------------------------------------------------------------------------------------------
-constexpr size_t kRowsLdsMax = 120 * 1024;
+constexpr size_t kRowsLdsMax = 160 * 1024;  // LDS per CU (static + dynamic)
 
-template <typename T, int MT, int PRO>
-static size_t rows_lds_bytes(const RowsGemmArgs& a) {
-  // the swizzled tile needs whole 256-byte rows; PRO_LN keeps K <= 1024 in registers;
-  // the logits history lives in 64-entry LDS rows
-  if ((a.K * sizeof(T)) % 256 != 0) return ~size_t(0);
-  if (PRO == PRO_LN && a.K > 1024) return ~size_t(0);
-  if (a.hist_ld > 64) return ~size_t(0);
-  return (size_t)MT * 16 * a.K * sizeof(T);
+template <typename T>
+constexpr bool gemv_nsl_ok(int nsl) {
+  return sizeof(T) == 2 ? (nsl == 6 || nsl == 8 || nsl == 24 || nsl == 32) : (nsl == 12 || nsl == 16);
+}
+// register budget: NSL x (NTB weight + MT activation) 16-byte fragments held at once
+template <typename T, int MT, int NTB, int PRO, int NSL>
+constexpr bool gemv_fits() {
+  constexpr int KS = 4 * Frag<T>::kElems;
+  return gemv_nsl_ok<T>(NSL) && NSL * (NTB + (PRO == PRO_DIRECT ? MT : 0)) <= 48 &&
+         (PRO != PRO_LN || NSL * KS * 4 <= 1024);
+}
+
+// Raise a kernel's dynamic-LDS limit once to what the CU has left beside its static LDS; returns
+// that limit (0 on error).
+template <typename Kern>
+static int allow_lds(Kern k, int& limit) {
+  if (limit > 0) return limit;
+  hipFuncAttributes attr;
+  if (hipFuncGetAttributes(&attr, (const void*)k) != hipSuccess) return 0;
+  const int dyn = (int)kRowsLdsMax - (int)attr.sharedSizeBytes;
+  if (dyn <= 0 || hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, dyn) != hipSuccess)
+    return 0;
+  limit = dyn;
+  return limit;
+}
+
+template <typename T, int MT, int NTB, int PRO, int EPI, int NSL>
+static hipError_t launch_gemv(const RowsGemmArgs& a, hipStream_t s) {
+  const dim3 grid((a.N + NTB * 16 - 1) / (NTB * 16), (a.M + MT * 16 - 1) / (MT * 16));
+  const size_t lds = PRO == PRO_LN ? (size_t)MT * 16 * a.K * sizeof(T) : 0;
+  static int limit = 0;
+  if ((size_t)allow_lds(vcap_rows_gemv_kernel<T, MT, NTB, PRO, EPI, NSL>, limit) < lds) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((vcap_rows_gemv_kernel<T, MT, NTB, PRO, EPI, NSL>), grid, dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, int MT, int NTB, int PRO, int EPI>
+static hipError_t launch_generic(const RowsGemmArgs& a, hipStream_t s) {
+  const dim3 grid((a.N + NTB * 16 - 1) / (NTB * 16), (a.M + MT * 16 - 1) / (MT * 16));
+  const size_t lds = PRO == PRO_LN ? (size_t)MT * 16 * a.K * sizeof(T) : 0;
+  static int limit = 0;
+  if ((size_t)allow_lds(vcap_rows_gemm_lds_kernel<T, MT, NTB, PRO, EPI>, limit) < lds) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((vcap_rows_gemm_lds_kernel<T, MT, NTB, PRO, EPI>), grid, dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, int MT, int NTB, int PRO, int EPI, int NSL>
+static bool try_gemv(int nsl, const RowsGemmArgs& a, hipStream_t s, hipError_t& err) {
+  if constexpr (gemv_fits<T, MT, NTB, PRO, NSL>()) {
+    if (nsl == NSL) {
+      err = launch_gemv<T, MT, NTB, PRO, EPI, NSL>(a, s);
+      return true;
+    }
+  }
+  return false;
 }
 
 template <typename T, int MT, int NTB, int PRO, int EPI>
 static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
-  const int nblk = (a.N + NTB * 16 - 1) / (NTB * 16);
-  const size_t lds = rows_lds_bytes<T, MT, PRO>(a);
-  if (lds <= kRowsLdsMax) {
-    static bool configured = false;
-    if (!configured) {
-      hipError_t e = hipFuncSetAttribute((const void*)vcap_rows_gemm_lds_kernel<T, MT, NTB, PRO, EPI>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRowsLdsMax);
-      if (e != hipSuccess) return e;
-      configured = true;
-    }
-    hipLaunchKernelGGL((vcap_rows_gemm_lds_kernel<T, MT, NTB, PRO, EPI>), dim3(nblk), dim3(256), lds, s, a);
-  } else {
-    hipLaunchKernelGGL((vcap_rows_gemm_kernel<T, MT, NTB, PRO, EPI>), dim3(nblk), dim3(256), 0, s, a);
-  }
-  return hipGetLastError();
+  const int nsl = a.K / (16 * Frag<T>::kElems);
+  hipError_t err = hipSuccess;
+  if (try_gemv<T, MT, NTB, PRO, EPI, 6>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 8>(nsl, a, s, err) ||
+      try_gemv<T, MT, NTB, PRO, EPI, 12>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 16>(nsl, a, s, err) ||
+      try_gemv<T, MT, NTB, PRO, EPI, 24>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 32>(nsl, a, s, err))
+    return err;
+  return launch_generic<T, MT, NTB, PRO, EPI>(a, s);
 }
 
-template <typename T, int PRO, int EPI, int NTB>
-static hipError_t launch_rows_mt(const RowsGemmArgs& a, hipStream_t s) {
-  const int mt = (a.M + 15) / 16;
-  if (mt <= 1) return launch_rows<T, 1, NTB, PRO, EPI>(a, s);
-  if (mt <= 2) return launch_rows<T, 2, NTB, PRO, EPI>(a, s);
-  if constexpr (NTB <= 2) {
-    if (mt <= 4) return launch_rows<T, 4, NTB, PRO, EPI>(a, s);
-  }
-  if constexpr (NTB <= 1) {
-    if (mt <= 8) return launch_rows<T, 8, NTB, PRO, EPI>(a, s);
-  }
-  return hipErrorInvalidValue;
-}
-
-static int rows_ntb(int epi, int M) {
-  const int mt = (M + 15) / 16;
-  return (epi == EPI_LOGITS) ? (mt <= 2 ? 4 : (mt <= 4 ? 2 : 1)) : 1;
-}
+static int rows_ntb(int epi) { return epi == EPI_LOGITS ? 4 : 1; }
 
 int vcap_logit_blocks(int V, int M) {
-  const int ntb = rows_ntb(EPI_LOGITS, M);
+  (void)M;
+  const int ntb = rows_ntb(EPI_LOGITS);
   return (V + ntb * 16 - 1) / (ntb * 16);
 }
 
-// Public dispatcher: picks NTB so the whole M fits (MT*NTB <= 8); logits prefer wide tiles.
+// Public dispatcher.  Rows go in chunks of MT*16 over blockIdx.y (MT = 1 for M <= 16, else 2).
 hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs& a, int* nblk_out, hipStream_t s) {
-  if (a.K % 64 != 0 || a.M <= 0 || a.M > 128) return hipErrorInvalidValue;
-  const int ntb = rows_ntb(epi, a.M);
+  const int ks4 = dt == VCAP_DT_BF16 ? 128 : 64;  // 4 waves x one MFMA K step
+  if (a.K % ks4 != 0 || a.M <= 0 || a.K <= 0 || a.N <= 0) return hipErrorInvalidValue;
+  if (pro == PRO_LN && a.K > 1024) return hipErrorInvalidValue;
+  if (epi == EPI_LOGITS && a.hist_ld > 64) return hipErrorInvalidValue;
+  const int ntb = rows_ntb(epi);
   if (nblk_out) *nblk_out = (a.N + ntb * 16 - 1) / (ntb * 16);
-#define VCAP_ROWS_CASE(TT, PP, EE)                                          \
-  if (ntb == 4) return launch_rows_mt<TT, PP, EE, 4>(a, s);                \
-  if (ntb == 2) return launch_rows_mt<TT, PP, EE, 2>(a, s);                \
-  return launch_rows_mt<TT, PP, EE, 1>(a, s);
-#define VCAP_ROWS_EPI(TT)                                                                   \
-  if (pro == PRO_LN && epi == EPI_QKV) { VCAP_ROWS_CASE(TT, PRO_LN, EPI_QKV) }             \
-  if (pro == PRO_LN && epi == EPI_GELU) { VCAP_ROWS_CASE(TT, PRO_LN, EPI_GELU) }           \
-  if (pro == PRO_DIRECT && epi == EPI_RESID) { VCAP_ROWS_CASE(TT, PRO_DIRECT, EPI_RESID) } \
-  if (pro == PRO_DIRECT && epi == EPI_LOGITS) { VCAP_ROWS_CASE(TT, PRO_DIRECT, EPI_LOGITS) } \
-  if (pro == PRO_DIRECT && epi == EPI_STORE) { VCAP_ROWS_CASE(TT, PRO_DIRECT, EPI_STORE) } \
-  if (pro == PRO_LN && epi == EPI_STORE) { VCAP_ROWS_CASE(TT, PRO_LN, EPI_STORE) }
+  const bool one = a.M <= 16;
+#define VCAP_ROWS(TT, PP, EE, NT) \
+  return one ? launch_rows<TT, 1, NT, PP, EE>(a, s) : launch_rows<TT, 2, NT, PP, EE>(a, s);
+#define VCAP_ROWS_EPI(TT)                                                                     \
+  if (pro == PRO_LN && epi == EPI_QKV) { VCAP_ROWS(TT, PRO_LN, EPI_QKV, 1) }                 \
+  if (pro == PRO_LN && epi == EPI_GELU) { VCAP_ROWS(TT, PRO_LN, EPI_GELU, 1) }               \
+  if (pro == PRO_DIRECT && epi == EPI_RESID) { VCAP_ROWS(TT, PRO_DIRECT, EPI_RESID, 1) }     \
+  if (pro == PRO_LN && epi == EPI_LOGITS) { VCAP_ROWS(TT, PRO_LN, EPI_LOGITS, 4) }
   if (dt == VCAP_DT_BF16) {
     VCAP_ROWS_EPI(bf16_t)
   } else {
     VCAP_ROWS_EPI(float)
   }
 #undef VCAP_ROWS_EPI
-#undef VCAP_ROWS_CASE
+#undef VCAP_ROWS
   return hipErrorInvalidValue;
+}
+
+hipError_t vcap_rows_pack_dispatch(int dt, const void* w, long ldw, int N, int K, void* packed, hipStream_t s) {
+  const int ks = dt == VCAP_DT_BF16 ? 32 : 16;
+  const size_t esz = dt == VCAP_DT_BF16 ? 2 : 4;
+  if (N <= 0 || K <= 0 || K % ks != 0 || (ldw * esz) % 16 != 0 || ((uintptr_t)w & 15) || ((uintptr_t)packed & 15))
+    return hipErrorInvalidValue;
+  const long chunks = (long)((N + 15) / 16) * (K / ks) * 64;
+  const int blocks = (int)std::min<long>((chunks + 255) / 256, 4096);
+  if (dt == VCAP_DT_BF16)
+    hipLaunchKernelGGL((vcap_rows_pack_kernel<bf16_t>), dim3(blocks), dim3(256), 0, s, (const bf16_t*)w, ldw, N, K,
+                       (u32x4*)packed);
+  else
+    hipLaunchKernelGGL((vcap_rows_pack_kernel<float>), dim3(blocks), dim3(256), 0, s, (const float*)w, ldw, N, K,
+                       (u32x4*)packed);
+  return hipGetLastError();
+}
+
+size_t vcap_rows_packed_size(int dt, int N, int K) {
+  const int ks = dt == VCAP_DT_BF16 ? 32 : 16;
+  return (size_t)((N + 15) / 16) * (size_t)(K / ks) * 1024;
 }
 
 hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc, const void* vc, const int* pt,
                                           int maxp, void* out, int M, int H, int S_new, int past, hipStream_t s) {
-  if (past + S_new > 1024) return hipErrorInvalidValue;
+  if (past + S_new > 1024 || maxp > 64) return hipErrorInvalidValue;
   const dim3 grid((M * H + 3) / 4), block(256);
   if (dt == VCAP_DT_BF16)
     hipLaunchKernelGGL((vcap_decode_attention_kernel<bf16_t>), grid, block, 0, s, (const bf16_t*)q,
@@ -832,6 +867,7 @@ hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const in
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,
                                          const float* wpe, float* h, int E, int pos_next, int vocab, hipStream_t s) {
+  if (hist_ld > 1024) return hipErrorInvalidValue;
   if (dt == VCAP_DT_BF16)
     hipLaunchKernelGGL((vcap_decode_finalize_kernel<bf16_t>), dim3(B), dim3(256), 0, s, part_val, part_idx, nblk,
                        step, finished, hist, hist_ld, banned, nbanned, ngram, eos, pad, out_ids, out_ld,

@@ -132,7 +132,6 @@ struct DecBufs {
   void* q;
   void* attn;
   void* act;
-  void* xn;
   void* kc;
   void* vc;
   int* pt;
@@ -160,7 +159,6 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.q = c.take(Mmax * E * es);
   b.attn = c.take(Mmax * E * es);
   b.act = c.take(Mmax * 4 * E * es);
-  b.xn = c.take((size_t)B * E * es);
   b.kc = c.take(per_layer * d->n_layer * es);
   b.vc = c.take(per_layer * d->n_layer * es);
   b.pt = (int*)c.take(pages * 4);
@@ -178,7 +176,16 @@ int check_gpt2(const vcap_gpt2_desc* d) {
   if (!d || !d->layers) return fail(VCAP_E_ARG, "gpt2 desc is null");
   if (d->dtype != VCAP_DT_F32 && d->dtype != VCAP_DT_BF16) return fail(VCAP_E_ARG, "gpt2 dtype");
   if (d->n_head * 64 != d->n_embd) return fail(VCAP_E_UNSUPPORTED, "gpt2 head_dim must be 64");
-  if (d->n_embd % 64) return fail(VCAP_E_UNSUPPORTED, "n_embd must be a multiple of 64");
+  if (d->n_embd % 128) return fail(VCAP_E_UNSUPPORTED, "n_embd must be a multiple of 128");
+  if (d->n_embd > 1024) return fail(VCAP_E_UNSUPPORTED, "n_embd > 1024 (LayerNorm rows are held in registers)");
+  return 0;
+}
+
+// shape checks + the weight pointers a launch dereferences
+int check_gpt2_launch(const vcap_gpt2_desc* d) {
+  if (int rc = check_gpt2(d)) return rc;
+  if (!d->lm_head || !d->wte || !d->wpe || !d->lnf_g || !d->lnf_b)
+    return fail(VCAP_E_ARG, "gpt2 wte / lm_head / wpe / ln_f pointer is null");
   return 0;
 }
 
@@ -195,7 +202,7 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     a.ln_eps = d->ln_eps;
     // 1) ln_1 + c_attn -> q, paged K/V
     a.x = w.h; a.ldx = E; a.ln_g = ly.ln1_g; a.ln_b = ly.ln1_b;
-    a.w = ly.attn_w; a.ldw = E; a.bias = ly.attn_b; a.N = 3 * E; a.K = E;
+    a.w = ly.attn_w; a.bias = ly.attn_b; a.N = 3 * E; a.K = E;
     a.q_out = w.q;
     a.kc = (char*)w.kc + (size_t)l * page_elems * es;
     a.vc = (char*)w.vc + (size_t)l * page_elems * es;
@@ -207,42 +214,41 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     // 3) attn c_proj + residual
     RowsGemmArgs b;
     memset(&b, 0, sizeof(b));
-    b.M = M; b.x = w.attn; b.ldx = E; b.w = ly.aproj_w; b.ldw = E; b.bias = ly.aproj_b; b.N = E; b.K = E;
+    b.M = M; b.x = w.attn; b.ldx = E; b.w = ly.aproj_w; b.bias = ly.aproj_b; b.N = E; b.K = E;
     b.out = w.h; b.ldo = E;
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, b, nullptr, s), "attn_c_proj");
     // 4) ln_2 + c_fc + gelu_new
     RowsGemmArgs c;
     memset(&c, 0, sizeof(c));
     c.M = M; c.x = w.h; c.ldx = E; c.ln_g = ly.ln2_g; c.ln_b = ly.ln2_b; c.ln_eps = d->ln_eps;
-    c.w = ly.fc_w; c.ldw = E; c.bias = ly.fc_b; c.N = 4 * E; c.K = E; c.out = w.act; c.ldo = 4 * E;
+    c.w = ly.fc_w; c.bias = ly.fc_b; c.N = 4 * E; c.K = E; c.out = w.act; c.ldo = 4 * E;
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_GELU, c, nullptr, s), "c_fc");
     // 5) mlp c_proj + residual
     RowsGemmArgs e;
     memset(&e, 0, sizeof(e));
-    e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.ldw = 4 * E; e.bias = ly.mproj_b; e.N = E;
+    e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.bias = ly.mproj_b; e.N = E;
     e.K = 4 * E; e.out = w.h; e.ldo = E;
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, e, nullptr, s), "mlp_c_proj");
   }
   return 0;
 }
 
-// ln_f on each sequence's last row + tied lm_head with the fused processors and argmax partials.
+// ln_f on each sequence's last row (fused into the lm_head's A prologue) + tied lm_head with the
+// fused processors and argmax partials.
 int run_lm_head(const vcap_gpt2_desc* d, const DecBufs& w, int rows, int S_new, float* logits_raw, int hist_ld,
                 int gen_len, float rep, int min_new, int eos, int* nblk, hipStream_t s) {
   const int E = d->n_embd;
-  const int dt = d->dtype;
-  VCAP_TRY(vcap_layernorm_dispatch(dt, w.h + (size_t)(S_new - 1) * E, (long)S_new * E, w.xn, E, d->lnf_g, d->lnf_b,
-                                   rows, E, d->ln_eps, s),
-           "ln_f");
   RowsGemmArgs g;
   memset(&g, 0, sizeof(g));
-  g.M = rows; g.x = w.xn; g.ldx = E; g.w = d->wte; g.ldw = E; g.bias = nullptr; g.N = d->vocab; g.K = E;
+  g.M = rows; g.x = w.h + (size_t)(S_new - 1) * E; g.ldx = (long)S_new * E;
+  g.ln_g = d->lnf_g; g.ln_b = d->lnf_b; g.ln_eps = d->ln_eps;
+  g.w = d->lm_head; g.bias = nullptr; g.N = d->vocab; g.K = E;
   g.logits_raw = logits_raw;
   g.part_val = w.pval; g.part_idx = w.pidx;
   g.nblk = max_logit_blocks(d->vocab, rows);
   g.hist = w.hist; g.hist_ld = hist_ld; g.gen_len = gen_len; g.banned = w.banned; g.nbanned = w.nbanned;
   g.rep_penalty = rep; g.min_new = min_new; g.eos = eos;
-  VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_LOGITS, g, nblk, s), "lm_head");
+  VCAP_TRY(vcap_rows_gemm_dispatch(d->dtype, PRO_LN, EPI_LOGITS, g, nblk, s), "lm_head");
   return 0;
 }
 
@@ -436,6 +442,20 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
   return 0;
 }
 
+size_t vcap_rows_packed_bytes(int dtype, int N, int K) {
+  if (dtype != VCAP_DT_F32 && dtype != VCAP_DT_BF16) return 0;
+  if (N <= 0 || K <= 0 || K % (dtype == VCAP_DT_BF16 ? 32 : 16)) return 0;
+  return vcap_rows_packed_size(dtype, N, K);
+}
+
+int vcap_rows_pack(int dtype, const void* w, int64_t ldw, int N, int K, void* packed, void* stream) {
+  if (dtype != VCAP_DT_F32 && dtype != VCAP_DT_BF16) return fail(VCAP_E_ARG, "rows_pack dtype");
+  if (!w || !packed || ldw < K) return fail(VCAP_E_ARG, "rows_pack: null pointer or ldw < K");
+  VCAP_TRY(vcap_rows_pack_dispatch(dtype, w, (long)ldw, N, K, packed, (hipStream_t)stream),
+           "rows_pack (K % 32/16, 16-byte aligned rows and pointers)");
+  return 0;
+}
+
 size_t vcap_gpt2_workspace_bytes(const vcap_gpt2_desc* d, int B, int S0, int max_new_tokens) {
   if (check_gpt2(d)) return 0;
   Carver c(nullptr);
@@ -448,10 +468,12 @@ size_t vcap_gpt2_workspace_bytes(const vcap_gpt2_desc* d, int B, int S0, int max
 int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* prompt_ids,
                        int prompt_len, int B, int* out_ids, float* logits_out, void* workspace, size_t ws_bytes,
                        void* stream) {
-  if (int rc = check_gpt2(d)) return rc;
+  if (int rc = check_gpt2_launch(d)) return rc;
   if (!gp || !prefix || !out_ids || B <= 0 || prompt_len < 0 || prompt_len > 64 || (prompt_len && !prompt_ids))
     return fail(VCAP_E_ARG, "vcap_gpt2_generate: bad arguments");
   if (gp->max_new_tokens <= 0) return fail(VCAP_E_ARG, "max_new_tokens must be > 0");
+  if (gp->max_new_tokens > 64)
+    return fail(VCAP_E_UNSUPPORTED, "max_new_tokens > 64 (the lm_head stages the processors' history in LDS)");
   const int S0 = d->prefix_len + prompt_len;
   if (S0 <= 0 || B * S0 > 128) return fail(VCAP_E_UNSUPPORTED, "B*(prefix+prompt) must be <= 128 rows");
   if (S0 + gp->max_new_tokens > d->n_positions || S0 + gp->max_new_tokens > 1024)
@@ -546,7 +568,7 @@ size_t vcap_gpt2_beam_workspace_bytes(const vcap_gpt2_desc* d, int rows, int S0,
 
 static int step_setup(const vcap_gpt2_desc* d, int rows, int S0, int max_new, void* ws, size_t ws_bytes, DecBufs* w,
                       int* maxp, size_t* pe, void** scratch) {
-  if (int rc = check_gpt2(d)) return rc;
+  if (int rc = check_gpt2_launch(d)) return rc;
   if (rows <= 0 || rows > 128 || S0 <= 0 || max_new <= 0 || S0 + max_new > d->n_positions)
     return fail(VCAP_E_ARG, "gpt2 step: bad rows / lengths");
   if (ws_bytes < vcap_gpt2_beam_workspace_bytes(d, rows, S0, max_new))

@@ -21,8 +21,7 @@ struct RowsGemmArgs {
   const float* ln_g;
   const float* ln_b;
   float ln_eps;
-  const void* w;  // T [N, K]
-  long ldw;
+  const void* w;  // rows-packed T weights of a [N, K] matrix (vcap_rows_pack_dispatch)
   const float* bias;
   int M, N, K;
   void* out;  // RESID: f32 [M, ldo] (+=); GELU/STORE: T [M, ldo]
@@ -61,6 +60,8 @@ hipError_t vcap_vit_head_prefix_dispatch(const float* x, int B, int T, int N, in
 hipError_t vcap_vit_pool_dispatch(int dt, const void* x, void* y, int B, int T, int tokens, int C, int gap,
                                   hipStream_t s);
 hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs& a, int* nblk_out, hipStream_t s);
+hipError_t vcap_rows_pack_dispatch(int dt, const void* w, long ldw, int N, int K, void* packed, hipStream_t s);
+size_t vcap_rows_packed_size(int dt, int N, int K);
 int vcap_logit_blocks(int V, int M);
 hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc, const void* vc, const int* pt,
                                           int maxp, void* out, int M, int H, int S_new, int past, hipStream_t s);

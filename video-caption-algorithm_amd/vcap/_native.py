@@ -16,7 +16,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
 DT_F32, DT_BF16 = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
@@ -50,7 +50,7 @@ class GPT2Layer(C.Structure):
 
 class GPT2Desc(C.Structure):
     _fields_ = [("dtype", i32), ("n_embd", i32), ("n_layer", i32), ("n_head", i32), ("vocab", i32),
-                ("n_positions", i32), ("prefix_len", i32), ("ln_eps", f32), ("wte", vp), ("wpe", vp),
+                ("n_positions", i32), ("prefix_len", i32), ("ln_eps", f32), ("wte", vp), ("lm_head", vp), ("wpe", vp),
                 ("lnf_g", vp), ("lnf_b", vp), ("layers", C.POINTER(GPT2Layer))]
 
 
@@ -70,6 +70,8 @@ SIGNATURES = {
     "vcap_vit_attention": (i32, [i32, vp, vp, i32, i32, i32, vp]),
     "vcap_vit_pool_temporal": (i32, [i32, vp, vp, i32, i32, i32, i32, i32, vp]),
     "vcap_prefix_project": (i32, [vp, i32, i32, C.POINTER(PrefixDesc), vp, vp]),
+    "vcap_rows_packed_bytes": (sz, [i32, i32, i32]),
+    "vcap_rows_pack": (i32, [i32, vp, i64, i32, i32, vp, vp]),
     "vcap_vit_workspace_bytes": (sz, [C.POINTER(VitDesc), i32, i32]),
     "vcap_vit_encode": (i32, [C.POINTER(VitDesc), C.POINTER(PrefixDesc), vp, i32, i32, vp, vp, vp, sz, vp]),
     "vcap_gpt2_workspace_bytes": (sz, [C.POINTER(GPT2Desc), i32, i32, i32]),

@@ -207,15 +207,14 @@ class HipGPT2Decoder:
             self._keep.append(t)
             return t
 
-        def conv_t(k):  # Conv1D [in, out] -> [out, in]
+        def conv_t(k):  # Conv1D [in, out] -> [out, in] -> rows-packed (vcap_rows_pack)
             t = torch.from_numpy(np.ascontiguousarray(sd[k], dtype=np.float32)).t().contiguous()
-            t = t.to(dev).to(tdt).contiguous()
-            self._keep.append(t)
-            return t
+            return self._pack(t.to(dev).to(tdt).contiguous())
 
         self.wte = torch.from_numpy(np.ascontiguousarray(sd[p + "wte.weight"], np.float32)).to(dev).to(tdt)
         self.wte = self.wte.contiguous()
         self._keep.append(self.wte)
+        self.lm_head = self._pack(self.wte)   # tied lm_head, packed copy
         self.wpe = f32(p + "wpe.weight")
         lnf_g, lnf_b = f32(p + "ln_f.weight"), f32(p + "ln_f.bias")
         self.layers = (N.GPT2Layer * arch.n_layer)()
@@ -232,9 +231,23 @@ class HipGPT2Decoder:
             ly.mproj_b = f32(b + "mlp.c_proj.bias").data_ptr()
         self.desc = N.GPT2Desc(dtype=self.dt, n_embd=arch.n_embd, n_layer=arch.n_layer, n_head=arch.n_head,
                                vocab=arch.vocab, n_positions=arch.n_positions, prefix_len=prefix_len,
-                               ln_eps=arch.ln_eps, wte=self.wte.data_ptr(), wpe=self.wpe.data_ptr(),
+                               ln_eps=arch.ln_eps, wte=self.wte.data_ptr(), lm_head=self.lm_head.data_ptr(),
+                               wpe=self.wpe.data_ptr(),
                                lnf_g=lnf_g.data_ptr(), lnf_b=lnf_b.data_ptr(), layers=self.layers)
         self.ws = _Workspace(dev)
+        torch.cuda.synchronize(dev)   # packing ran on the current stream; decodes may use others
+
+    def _pack(self, w: torch.Tensor) -> torch.Tensor:
+        """[N, K] device weight -> rows-packed copy (MFMA-fragment order, csrc/decode.hip)."""
+        rows, k = w.shape
+        nbytes = int(N.lib().vcap_rows_packed_bytes(self.dt, rows, k))
+        if nbytes == 0:
+            raise ValueError(f"cannot pack a [{rows}, {k}] weight (K must be a multiple of 32 bf16 / 16 f32)")
+        packed = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+        N.check(N.lib().vcap_rows_pack(self.dt, w.data_ptr(), w.stride(0), rows, k, packed.data_ptr(),
+                                       _stream(w.device)), "vcap_rows_pack")
+        self._keep.append(packed)
+        return packed
 
     def workspace_bytes(self, B: int, prompt_len: int, max_new: int) -> int:
         return int(N.lib().vcap_gpt2_workspace_bytes(C.byref(self.desc), B, self.prefix_len + prompt_len, max_new))

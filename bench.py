@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="no encode/decode overlap (each step's decode finishes before the next encode starts)")
+    ap.add_argument("--reserve-cus", type=int, default=0,
+                    help="CUs the encode stream leaves to the decode stream (CU-masked stream; 0 = none)")
     ap.add_argument("--cpu-baseline-s", type=float, default=20.0, help="CPU oracle time budget (0 disables)")
     return ap.parse_args()
 
@@ -111,7 +113,8 @@ def main():
     else:
         cfg = GenConfig.raw_greedy(args.max_new, ga.eos_token_id, not args.no_graph)
     gather = (lambda ids: gather_ids(ids, world)) if world > 1 else None
-    pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev, gather=gather)
+    pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev, gather=gather,
+                           reserve_cus=0 if args.serial else args.reserve_cus)
 
     def step(t0=None, t1=None, t2=None):
         pipe.submit(video, t0, t1, t2)
@@ -177,7 +180,9 @@ def main():
                        "vit": args.vit, "gpt2": args.gpt2, "batch_per_gpu": B, "global_batch": world * B,
                        "frames": T, "max_new_tokens": args.max_new, "decode": args.decode,
                        "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}",
-                       "schedule": "serial" if args.serial else "encode(k+1) overlapped with decode(k) on 2 HIP streams"},
+                       "schedule": "serial" if args.serial else
+                       f"encode(k+1) overlapped with decode(k) on 2 HIP streams (encode CU-masked off "
+                       f"{args.reserve_cus} CUs)"},
             "p50_latency_ms": p50,
             "stage_ms_p50": {"vit_encode_prefix": statistics.median(vit_ms),
                              "prefix_ready_to_ids": statistics.median(dec_ms)},
@@ -196,6 +201,7 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    pipe.close()
     if world > 1:
         dist.destroy_process_group()
 

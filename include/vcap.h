@@ -109,6 +109,18 @@ typedef struct vcap_gen_params {
 const char* vcap_last_error(void);
 int vcap_abi_version(void);
 
+/* ---- tuning: which ViT GEMM kernel vcap_gemm / vcap_vit_encode use (process-wide):
+ *      0 auto (256x256-tile kernel when the shape yields >= 512 tiles), 1 128x128 only,
+ *      2 256x256 wherever its shape constraints hold.  Results are identical up to fp32
+ *      summation order within a tile (both accumulate K in the same order). ---- */
+int vcap_set_gemm_policy(int policy);
+
+/* ---- a stream whose kernels avoid `reserve_cus` CUs (hipExtStreamCreateWithCUMask), so a
+ *      latency-bound chain on another stream (the decode graph) always finds free CUs while
+ *      the MFMA-bound encode fills the rest.  Destroy with vcap_stream_destroy. ---- */
+int vcap_stream_create_cu_reserved(int reserve_cus, void** stream);
+int vcap_stream_destroy(void* stream);
+
 /* ---- op-level entry points ---- */
 int vcap_linear_bias(int dtype, const void* x, const void* w, const float* b, void* y, int rows, int in_features,
                      int out_features, void* stream);

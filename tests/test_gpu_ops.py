@@ -24,9 +24,19 @@ def _rand(shape, seed, scale=1.0, device="cuda"):
     return (torch.randn(*shape, generator=g) * scale).to(device)
 
 
+@pytest.fixture(params=[1, 2], ids=["tile128", "tile256"])
+def gemm_policy(request):
+    """Run a GEMM test with the 128x128 kernel and again with the 256x256 8-phase kernel forced
+    wherever its shape constraints hold (vcap_set_gemm_policy)."""
+    N.check(N.lib().vcap_set_gemm_policy(request.param), "policy")
+    yield request.param
+    N.check(N.lib().vcap_set_gemm_policy(0), "policy")
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-@pytest.mark.parametrize("M,N_,K", [(300, 384, 256), (128, 128, 64), (1, 2304, 768), (197, 200, 192)])
-def test_gemm_plain_bias(device, prec, M, N_, K):
+@pytest.mark.parametrize("M,N_,K", [(300, 384, 256), (128, 128, 64), (1, 2304, 768), (197, 200, 192),
+                                    (3152, 2304, 768), (1000, 768, 3072), (257, 272, 128)])
+def test_gemm_plain_bias(device, gemm_policy, prec, M, N_, K):
     dt, tdt = (N.DT_F32, torch.float32) if prec == "fp32" else (N.DT_BF16, torch.bfloat16)
     if prec == "bf16" and K % 64:
         pytest.skip("bf16 K step is 64")
@@ -42,7 +52,7 @@ def test_gemm_plain_bias(device, prec, M, N_, K):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-def test_gemm_gelu_and_residual(device, prec):
+def test_gemm_gelu_and_residual(device, gemm_policy, prec):
     dt, tdt = (N.DT_F32, torch.float32) if prec == "fp32" else (N.DT_BF16, torch.bfloat16)
     M, N_, K = 333, 256, 128
     A = _rand((M, K), 4).to(tdt)
@@ -63,7 +73,7 @@ def test_gemm_gelu_and_residual(device, prec):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-def test_gemm_patch_remap_pos(device, prec):
+def test_gemm_patch_remap_pos(device, gemm_policy, prec):
     """Patch-embed epilogue: out row (m/P)*(P+1)+1+m%P, + bias + pos[1 + m%P]."""
     dt, tdt = (N.DT_F32, torch.float32) if prec == "fp32" else (N.DT_BF16, torch.bfloat16)
     BT, P, D, K = 3, 196, 128, 768

@@ -170,9 +170,18 @@ static hipError_t launch_gemm(const void* A, long lda, const void* W, long ldw, 
   return launch_gemm_epi<TIn, TOut, 3>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
 }
 
+static int g_gemm_policy = 0;  // 0 auto, 1 always the 128x128 kernel, 2 the 256x256 kernel where it applies
+void vcap_gemm_set_policy(int p) { g_gemm_policy = p; }
+
 // in_dt: operand dtype; out_dt: C dtype (the residual stream is f32)
 hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
                               long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s) {
+  if (g_gemm_policy != 1 && vcap_gemm256_ok(in_dt, out_dt, lda, ldw, ldc, M, N, K, epi)) {
+    // 256x256 tiles need enough of them to fill the chip (one workgroup per CU)
+    const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+    if (g_gemm_policy == 2 || tiles256 >= 512)
+      return vcap_gemm256_dispatch(in_dt, out_dt, A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  }
   if (in_dt == VCAP_DT_BF16 && out_dt == VCAP_DT_BF16)
     return launch_gemm<bf16_t, bf16_t>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
   if (in_dt == VCAP_DT_BF16 && out_dt == VCAP_DT_F32)

@@ -1,0 +1,322 @@
+// 256x256-tile MFMA GEMM for the ViT projections (QKV, attn-proj, fc1, fc2, patch-embed):
+//   C[M,N] = epilogue( A[M,K] . W[N,K]^T )     (torch Linear layout, both operands K-contiguous)
+// Replaces the timm Linear layers the reference drives (src/models/video_encoder.py:162-172).
+//
+// Structure (CDNA4 8-phase software pipeline, one workgroup of 8 waves per CU):
+//  * tile 256x256, K step 64 bf16 (128 B per row), waves 2 (M) x 4 (N), 128x64 outputs per wave
+//    held as four 64x32 quadrants of 16x16 MFMA accumulators;
+//  * LDS (128 KiB, one dynamic array) = 2 K-tile buffers x {A-h0, A-h1, B-h0, B-h1}; a "half"
+//    holds the 128 rows that feed one quadrant row / column of every wave:
+//      A-hX local row l -> tile row (l>>6)*128 + X*64 + (l&63)
+//      B-hY local row l -> tile col (l>>5)*64  + Y*32 + (l&31)
+//    so each half is read in exactly ONE phase of its K-tile and can be restaged right after;
+//  * per K-tile 4 phases, each = ds_read one register subtile, issue one half-tile of a future
+//    K-tile (2 global_load_lds_dwordx4 per thread), barrier, 16 MFMAs on one quadrant, barrier:
+//        phase 1: read A-h0 + B-h0 -> quadrant (0,0)     phase 2: read B-h1 -> (0,1)
+//        phase 3: read A-h1        -> (1,1)              phase 4: (registers only) -> (1,0)
+//  * the two wave groups (wr = 0 / 1, one wave of each per SIMD) run staggered by one barrier:
+//    while one group issues its MFMAs the other issues its ds_reads and LDS-DMA.  With the
+//    stagger a half may be restaged only >= 2 phases after its last read, so the staging order
+//    over an iteration (K-tiles t, t+1; buffers even/odd) is
+//        p1 B-h1(t+1)  p2 A-h1(t+1)  p3 A-h0(t+2)  p4 B-h0(t+2) | vmcnt(4): t+1 landed
+//        p5 B-h1(t+2)  p6 A-h1(t+2)  p7 A-h0(t+3)  p8 B-h0(t+3) | vmcnt(4): t+2 landed
+//    (2 half-tiles in flight across every barrier); a staged buffer is read only in a phase
+//    after the counted wait and the barrier that follow it in both groups;
+//  * the MFMA takes the weight fragment as its A operand, so each lane ends up holding 4
+//    consecutive output COLUMNS of one row: vectorised bias / residual / store epilogue.
+#include "vcap_common.h"
+#include "vcap_kernels.h"
+
+namespace {
+
+constexpr int TM = 256, TN = 256, ROWB = 128;
+constexpr int HALF = 128 * ROWB;  // 16 KiB
+constexpr int BUF = 4 * HALF;     // one K-tile: A-h0 A-h1 B-h0 B-h1
+constexpr int LDS_BYTES = 2 * BUF;
+
+VCAP_DEV void glds16(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// Per-thread source byte offsets of one half (128 rows x 128 B) of a K-tile: wave w writes LDS
+// 1 KiB blocks 2w, 2w+1 (8 rows each, lane-linear) and the XOR swizzle (chunk ^ (row & 7)) is
+// applied on the source.  GS: log2 of the rows per wave-group (6 for A: 64 rows of each of 2
+// M-waves; 5 for B: 32 rows of each of 4 N-waves).  32-bit offsets from a uniform base keep
+// every global_load_lds in the SGPR-base + VGPR-offset form.
+template <typename T, int GS>
+VCAP_DEV void half_offsets(uint32_t (&off)[2], long ld, int rows, int base, int X, int wave, int lane) {
+  constexpr int E = Frag<T>::kElems;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int lr = (wave * 2 + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (lr & 7);
+    int gr = base + (lr >> GS) * (2 << GS) + X * (1 << GS) + (lr & ((1 << GS) - 1));
+    gr = gr < rows ? gr : rows - 1;
+    off[i] = (uint32_t)(((long)gr * ld + c * E) * (long)sizeof(T));
+  }
+}
+
+VCAP_DEV void stage_half(const char* base_k, const uint32_t (&off)[2], char* lds_half, int wave) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) glds16(base_k + off[i], lds_half + (wave * 2 + i) * 1024);
+}
+
+VCAP_DEV u32x4 frag(const char* half, int row, int chunk) {
+  return *reinterpret_cast<const u32x4*>(half + row * ROWB + ((chunk ^ (row & 7)) << 4));
+}
+
+VCAP_DEV void lds_fence() { asm volatile("" ::: "memory"); }
+
+}  // namespace
+
+template <typename TIn, typename TOut, int EPI>
+__global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict__ A, long lda,
+                                                           const TIn* __restrict__ W, long ldw, TOut* C, long ldc,
+                                                           int M, int N, int K, GemmEpi epi) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BK = ROWB / sizeof(TIn);
+
+  const int tiles_n = (N + TN - 1) / TN;
+  const int tiles_m = (M + TM - 1) / TM;
+  const int nwg = tiles_m * tiles_n;
+  // XCD-aware bijective remap: consecutive tile ids (same A row panel) land on one XCD's L2
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
+  const int m0 = (wgid / tiles_n) * TM, n0 = (wgid % tiles_n) * TN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS-DMA bases stay scalar
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  u32x4 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+
+  uint32_t offA[2][2], offB[2][2];
+  half_offsets<TIn, 6>(offA[0], lda, M, m0, 0, wave, lane);
+  half_offsets<TIn, 6>(offA[1], lda, M, m0, 1, wave, lane);
+  half_offsets<TIn, 5>(offB[0], ldw, N, n0, 0, wave, lane);
+  half_offsets<TIn, 5>(offB[1], ldw, N, n0, 1, wave, lane);
+  auto stA = [&](int X, int kt) {
+    stage_half((const char*)A + (long)kt * ROWB, offA[X], smem + (kt & 1) * BUF + X * HALF, wave);
+  };
+  auto stB = [&](int Y, int kt) {
+    stage_half((const char*)W + (long)kt * ROWB, offB[Y], smem + (kt & 1) * BUF + (2 + Y) * HALF, wave);
+  };
+  auto rdA = [&](u32x4 (&f)[4][2], int X, int kt) {
+    const char* h = smem + (kt & 1) * BUF + X * HALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) f[i][s] = frag(h, wr * 64 + i * 16 + fr, s * 4 + fg);
+  };
+  auto rdB = [&](u32x4 (&f)[2][2], int Y, int kt) {
+    const char* h = smem + (kt & 1) * BUF + (2 + Y) * HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) f[j][s] = frag(h, wc * 32 + j * 16 + fr, s * 4 + fg);
+  };
+  auto mma = [&](f32x4 (&c)[4][2], const u32x4 (&af)[4][2], const u32x4 (&bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) c[i][j] = mfma_frag(bf[j][s], af[i][s], c[i][j], (TIn*)nullptr);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_reads = [&]() {
+    lds_fence();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto end_phase = [&]() {
+    lds_fence();
+    __builtin_amdgcn_s_barrier();
+    lds_fence();
+  };
+
+  const int nk = K / BK;  // even, >= 2 (dispatcher)
+  // prologue: K-tile 0 complete; K-tile 1's A-h0, B-h0 in flight
+  stA(0, 0);
+  stB(0, 0);
+  stB(1, 0);
+  stA(1, 0);
+  stA(0, 1);
+  stB(0, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  end_phase();
+  // Stagger: the wr == 1 wave group runs one barrier behind, so on every SIMD one wave issues
+  // its MFMAs while the other issues ds_reads / LDS-DMA.  (Balanced by wr == 0 after the loop.)
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+
+  for (int t = 0; t < nk; t += 2) {
+    const bool more = t + 2 < nk;
+    // ---- K-tile t (even buffer)
+    rdB(b0, 0, t);
+    rdA(a0, 0, t);
+    stB(1, t + 1);
+    sync_reads();
+    mma(acc[0][0], a0, b0);
+    end_phase();
+
+    rdB(b1, 1, t);
+    stA(1, t + 1);
+    sync_reads();
+    mma(acc[0][1], a0, b1);
+    end_phase();
+
+    rdA(a1, 1, t);
+    if (more) stA(0, t + 2);
+    sync_reads();
+    mma(acc[1][1], a1, b1);
+    end_phase();
+
+    if (more) {
+      stB(0, t + 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // K-tile t+1 landed (this wave's part)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sync_reads();
+    mma(acc[1][0], a1, b0);
+    end_phase();
+
+    // ---- K-tile t+1 (odd buffer)
+    rdB(b0, 0, t + 1);
+    rdA(a0, 0, t + 1);
+    if (more) stB(1, t + 2);
+    sync_reads();
+    mma(acc[0][0], a0, b0);
+    end_phase();
+
+    rdB(b1, 1, t + 1);
+    if (more) stA(1, t + 2);
+    sync_reads();
+    mma(acc[0][1], a0, b1);
+    end_phase();
+
+    rdA(a1, 1, t + 1);
+    if (more) stA(0, t + 3);
+    sync_reads();
+    mma(acc[1][1], a1, b1);
+    end_phase();
+
+    if (more) {
+      stB(0, t + 3);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // K-tile t+2 landed
+    }
+    sync_reads();
+    mma(acc[1][0], a1, b0);
+    end_phase();
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+
+  // ---- epilogue: lane holds C[m][n .. n+3] of each 16x16 tile (m = .. + fr, n = .. + 4*fg)
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wc * 64 + qn * 32 + j * 16 + fg * 4;
+        if (n >= N) continue;
+        const f32x4 bias = epi.bias ? *reinterpret_cast<const f32x4*>(epi.bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wr * 128 + qm * 64 + i * 16 + fr;
+          if (m >= M) continue;
+          f32x4 v = acc[qm][qn][i][j] + bias;
+          long orow = m;
+          if constexpr (EPI == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+          } else if constexpr (EPI == 2) {
+            v += *reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n);
+          } else if constexpr (EPI == 3) {
+            if (epi.act == 1)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+            orow = epi.G ? (long)(m / epi.G) * epi.Gs + epi.goff + (m % epi.G) : (long)m;
+            if (epi.res_mode == 1) v += *reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n);
+            else if (epi.res_mode == 2)
+              v += *reinterpret_cast<const f32x4*>(epi.res + (long)((m % epi.G) + epi.roff) * epi.ldr + n);
+          }
+          if constexpr (sizeof(TOut) == 2) {
+            *reinterpret_cast<u32x2*>(C + orow * ldc + n) = (u32x2){pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
+          } else {
+            *reinterpret_cast<f32x4*>(C + orow * ldc + n) = v;
+          }
+        }
+      }
+}
+
+template <typename TIn, typename TOut, int EPI>
+static hipError_t launch256_epi(const void* A, long lda, const void* W, long ldw, void* C, long ldc, int M, int N,
+                                int K, const GemmEpi& epi, hipStream_t s) {
+  static bool configured = false;
+  if (!configured) {
+    hipError_t e = hipFuncSetAttribute((const void*)vcap_gemm256_kernel<TIn, TOut, EPI>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e != hipSuccess) return e;
+    configured = true;
+  }
+  const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  hipLaunchKernelGGL((vcap_gemm256_kernel<TIn, TOut, EPI>), dim3(tiles), dim3(512), LDS_BYTES, s, (const TIn*)A, lda,
+                     (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, epi);
+  return hipGetLastError();
+}
+
+template <typename TIn, typename TOut>
+static hipError_t launch256(const void* A, long lda, const void* W, long ldw, void* C, long ldc, int M, int N, int K,
+                            const GemmEpi& epi, hipStream_t s) {
+  const bool plain_rows = epi.G == 0;
+  if (plain_rows && epi.res_mode == 0 && epi.act == 0)
+    return launch256_epi<TIn, TOut, 0>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if constexpr (sizeof(TOut) == sizeof(TIn)) {
+    if (plain_rows && epi.res_mode == 0 && epi.act == 1)
+      return launch256_epi<TIn, TOut, 1>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  }
+  if constexpr (sizeof(TOut) == 4) {
+    if (plain_rows && epi.res_mode == 1 && epi.act == 0 && epi.res == (const float*)C && epi.ldr == ldc)
+      return launch256_epi<TIn, TOut, 2>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  }
+  return launch256_epi<TIn, TOut, 3>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+}
+
+// Shapes this kernel takes: K a multiple of two K-tiles, N and the strides in whole 16-byte
+// vectors for the epilogue, 16-byte aligned bias / residual rows.
+bool vcap_gemm256_ok(int in_dt, int out_dt, long lda, long ldw, long ldc, int M, int N, int K, const GemmEpi& epi) {
+  const int bk = in_dt == VCAP_DT_BF16 ? 64 : 32;
+  if (K % (2 * bk) != 0 || N % 16 != 0 || M <= 0) return false;
+  const int ein = in_dt == VCAP_DT_BF16 ? 8 : 4;
+  if (lda % ein || ldw % ein) return false;
+  if (ldc % 4) return false;
+  if (epi.bias && ((uintptr_t)epi.bias & 15)) return false;
+  if (epi.res && (((uintptr_t)epi.res & 15) || epi.ldr % 4)) return false;
+  (void)out_dt;
+  return true;
+}
+
+hipError_t vcap_gemm256_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
+                                 long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s) {
+  if (in_dt == VCAP_DT_BF16 && out_dt == VCAP_DT_BF16)
+    return launch256<bf16_t, bf16_t>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if (in_dt == VCAP_DT_BF16 && out_dt == VCAP_DT_F32)
+    return launch256<bf16_t, float>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if (in_dt == VCAP_DT_F32 && out_dt == VCAP_DT_F32)
+    return launch256<float, float>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  return hipErrorInvalidValue;
+}

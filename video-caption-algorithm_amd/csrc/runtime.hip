@@ -313,6 +313,34 @@ extern "C" {
 const char* vcap_last_error(void) { return g_err.c_str(); }
 int vcap_abi_version(void) { return VCAP_ABI_VERSION; }
 
+int vcap_stream_create_cu_reserved(int reserve_cus, void** stream) {
+  if (!stream || reserve_cus < 0) return fail(VCAP_E_ARG, "vcap_stream_create_cu_reserved: bad arguments");
+  int dev = 0;
+  VCAP_TRY(hipGetDevice(&dev), "hipGetDevice");
+  int ncu = 0;
+  VCAP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "cu count");
+  if (reserve_cus >= ncu) return fail(VCAP_E_ARG, "cannot reserve every CU");
+  // The driver spreads consecutive mask bits across XCDs / shader engines, so clearing the first
+  // `reserve_cus` bits leaves an even slice of every XCD to the other streams.
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  for (int c = reserve_cus; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
+  hipStream_t s = nullptr;
+  VCAP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
+  *stream = (void*)s;
+  return 0;
+}
+
+int vcap_stream_destroy(void* stream) {
+  VCAP_TRY(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
+  return 0;
+}
+
+int vcap_set_gemm_policy(int policy) {
+  if (policy < 0 || policy > 2) return fail(VCAP_E_ARG, "gemm policy must be 0 (auto), 1 (128x128) or 2 (256x256)");
+  vcap_gemm_set_policy(policy);
+  return 0;
+}
+
 int vcap_gemm(int in_dtype, int out_dtype, const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
               int64_t ldc, int M, int N, int K, const float* bias, int act, const float* res, int64_t ldr,
               int res_mode, int G, int Gs, int goff, int roff, void* stream) {
@@ -375,7 +403,8 @@ int vcap_prefix_project(const float* emb, int B, int video_dim, const vcap_prefi
   if (video_dim > 1024) return fail(VCAP_E_UNSUPPORTED, "video_dim > 1024");
   VCAP_TRY(vcap_vit_head_prefix_dispatch(nullptr, B, 1, 1, 1, nullptr, nullptr, 0.f, nullptr, nullptr, video_dim,
                                          pd->ln_scale, pd->in_weight, pd->mapper_w, pd->mapper_b,
-                                         pd->prefix_len * pd->n_embd, nullptr, prefix_out, emb, (hipStream_t)stream),
+                                         pd->prefix_len * pd->n_embd, nullptr, prefix_out, emb, nullptr,
+                                         (hipStream_t)stream),
            "vcap_prefix_project");
   return 0;
 }
@@ -437,7 +466,8 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
   const int MO = pd ? pd->prefix_len * pd->n_embd : 0;
   VCAP_TRY(vcap_vit_head_prefix_dispatch(w.x, B, T, N, D, d->norm_g, d->norm_b, d->ln_eps, d->proj_w, d->proj_b,
                                          d->video_dim, ls, iw, pd ? pd->mapper_w : nullptr,
-                                         pd ? pd->mapper_b : nullptr, MO, enc_out, prefix_out, nullptr, s),
+                                         pd ? pd->mapper_b : nullptr, MO, enc_out, prefix_out, nullptr,
+                                         (float*)w.xn, s),
            "head_prefix");
   return 0;
 }

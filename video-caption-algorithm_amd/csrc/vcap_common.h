@@ -37,11 +37,14 @@ template <> struct Num<bf16_t> {
 
 // tanh-approximate GELU, the form both torch's GELU(approximate="tanh")
 // (ViT MLP, src/models/video_encoder.py:123-134) and HF gelu_new (GPT-2 MLP) compute.
+// 0.5 x (1 + tanh(u)) == x * sigmoid(2u): one v_exp_f32 + one reciprocal instead of the
+// device-library tanhf (|error| ~1e-7 relative, far below the bf16 output rounding and the
+// fp32-mode tolerances).  exp overflow for very negative u gives x / inf = -0, the exact limit.
 VCAP_DEV float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
   const float k1 = 0.044715f;
-  float inner = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.0f + tanhf(inner));
+  const float u = k0 * (x + k1 * x * x * x);
+  return x * __frcp_rn(1.0f + __expf(-2.0f * u));
 }
 
 // Cross-lane reductions on the VALU: DPP within 16-lane rows, then the gfx950 permlane16/32

@@ -48,6 +48,10 @@ struct RowsGemmArgs {
 hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
                               long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s);
 int vcap_gemm_k_align(int in_dt);
+bool vcap_gemm256_ok(int in_dt, int out_dt, long lda, long ldw, long ldc, int M, int N, int K, const GemmEpi& epi);
+hipError_t vcap_gemm256_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
+                                 long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s);
+void vcap_gemm_set_policy(int p);
 hipError_t vcap_layernorm_dispatch(int out_dt, const float* x, long ldx, void* y, long ldy, const float* gamma,
                                    const float* beta, int rows, int D, float eps, hipStream_t s);
 hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s);
@@ -56,7 +60,7 @@ hipError_t vcap_patchify_dispatch(int dt, const float* frames, void* patches, fl
 hipError_t vcap_vit_head_prefix_dispatch(const float* x, int B, int T, int N, int D, const float* ng, const float* nb,
                                          float neps, const float* pw, const float* pb, int VD, float ln_scale,
                                          float in_weight, const float* mw, const float* mb, int MO, float* enc_out,
-                                         float* prefix, const float* emb_in, hipStream_t s);
+                                         float* prefix, const float* emb_in, float* emb_scratch, hipStream_t s);
 hipError_t vcap_vit_pool_dispatch(int dt, const void* x, void* y, int B, int T, int tokens, int C, int gap,
                                   hipStream_t s);
 hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs& a, int* nblk_out, hipStream_t s);

@@ -56,52 +56,47 @@ hipError_t vcap_patchify_dispatch(int dt, const float* frames, void* patches, fl
 }
 
 // ---------------------------------------------------------------------------------------------
-constexpr int HEAD_CHUNK = 256;  // mapper outputs per block
+// Encoder head + engine prefix, as two wide launches (every weight load of a wave issued before
+// its first reduction, so each phase costs ~one memory round trip):
+//   head:   pooled = mean_t LN_final(x[b, t, CLS]);  emb = pooled . proj_w^T + proj_b
+//           (video_encoder.py:316-326 CLS temporal pool + encoder.proj)      grid (B, VD/16)
+//   prefix: e = LN(emb) * ln_scale * in_weight (core/engine.py:44-50);
+//           prefix = e . mapper_w^T + mapper_b (text_decoder.py:249)         grid (B, MO/64)
+constexpr int HEAD_OUT = 16;    // proj outputs per head block (4 per wave)
+constexpr int PREFIX_OUT = 64;  // mapper outputs per prefix block (16 per wave, 4 at a time)
 
-__global__ __launch_bounds__(256) void vcap_vit_head_prefix_kernel(
-    const float* __restrict__ x, int T, int N, int D, const float* __restrict__ ng, const float* __restrict__ nb,
-    float neps, const float* __restrict__ pw, const float* __restrict__ pb, int VD, float ln_scale, float in_weight,
-    const float* __restrict__ mw, const float* __restrict__ mb, int MO, float* __restrict__ enc_out,
-    float* __restrict__ prefix, const float* __restrict__ emb_in) {
+__global__ __launch_bounds__(256) void vcap_vit_head_kernel(const float* __restrict__ x, int T, int N, int D,
+                                                            const float* __restrict__ ng, const float* __restrict__ nb,
+                                                            float neps, const float* __restrict__ pw,
+                                                            const float* __restrict__ pb, int VD,
+                                                            float* __restrict__ emb) {
   __shared__ float part[4][1024];
   __shared__ float pooled[1024];
-  __shared__ float emb[1024];
-  const int b = blockIdx.x, chunk = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-  if (emb_in) {  // vcap_prefix_project: start from a given encoder output
-    for (int o = tid; o < VD; o += 256) emb[o] = emb_in[(long)b * VD + o];
-    __syncthreads();
-    goto prefix_norm;
-  }
-  {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // 1) final LayerNorm of each frame's CLS row, summed over frames (per-wave partials)
   float accv[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) accv[i] = 0.f;
   for (int t = wave; t < T; t += 4) {
     const float* xr = x + ((long)(b * T + t) * N) * D;
-    float s = 0.f;
+    float xv[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int c = lane + 64 * i;
-      if (c < D) s += xr[c];
-    }
-    const float mean = wave_sum(s) / (float)D;
+    for (int i = 0; i < 16; ++i) xv[i] = xr[min(lane + 64 * i, D - 1)];  // clamped, never predicated
+    float sm = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sm += (lane + 64 * i < D) ? xv[i] : 0.f;
+    const float mean = wave_sum(sm) / (float)D;
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c = lane + 64 * i;
-      if (c < D) {
-        const float d = xr[c] - mean;
-        ss += d * d;
-      }
+      const float d = xv[i] - mean;
+      ss += (lane + 64 * i < D) ? d * d : 0.f;
     }
     const float rstd = rsqrtf(wave_sum(ss) / (float)D + neps);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c = lane + 64 * i;
-      if (c < D) accv[i] += (xr[c] - mean) * rstd * ng[c] + nb[c];
+      const int c = min(lane + 64 * i, D - 1);
+      accv[i] += (xv[i] - mean) * rstd * ng[c] + nb[c];
     }
   }
 #pragma unroll
@@ -112,64 +107,116 @@ __global__ __launch_bounds__(256) void vcap_vit_head_prefix_kernel(
   __syncthreads();
   for (int c = tid; c < D; c += 256) pooled[c] = (part[0][c] + part[1][c] + part[2][c] + part[3][c]) / (float)T;
   __syncthreads();
-
-  // 2) encoder.proj: emb[o] = pooled . pw[o] + pb[o]
-  for (int o = wave; o < VD; o += 4) {
-    const float* w = pw + (long)o * D;
-    float s = 0.f;
-    for (int c = lane; c < D; c += 64) s += pooled[c] * w[c];
-    s = wave_sum(s);
-    if (lane == 0) emb[o] = s + pb[o];
+  // 2) encoder.proj, 4 outputs per wave with all their weight loads in flight
+  const int ob = blockIdx.y * HEAD_OUT + wave * 4;
+  float sacc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < D; c0 += 256) {
+    float wv[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        wv[k][i] = pw[(long)min(ob + k, VD - 1) * D + min(c0 + lane + 64 * i, D - 1)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = c0 + lane + 64 * i;
+        if (c < D) sacc[k] += pooled[c] * wv[k][i];
+      }
   }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float v = wave_sum(sacc[k]);
+    if (lane == 0 && ob + k < VD) emb[(long)b * VD + ob + k] = v + pb[ob + k];
+  }
+}
+
+__global__ __launch_bounds__(256) void vcap_prefix_map_kernel(const float* __restrict__ emb_in, int VD, float ln_scale,
+                                                              float in_weight, const float* __restrict__ mw,
+                                                              const float* __restrict__ mb, int MO,
+                                                              float* __restrict__ prefix) {
+  __shared__ float emb[1024];
+  __shared__ float stat[2];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int c = tid; c < VD; c += 256) emb[c] = emb_in[(long)b * VD + c];
   __syncthreads();
-  if (chunk == 0 && enc_out)
-    for (int o = tid; o < VD; o += 256) enc_out[(long)b * VD + o] = emb[o];
-  }
-prefix_norm:
-  if (!prefix) return;
-
-  // 3) engine prefix normalisation (layer_norm without affine, eps 1e-5) * ln_scale, * in_weight
+  // engine prefix normalisation (layer_norm without affine, eps 1e-5) * ln_scale, * in_weight
   if (ln_scale > 0.f || in_weight > 0.f) {
     if (wave == 0) {
-      float s = 0.f;
-      for (int c = lane; c < VD; c += 64) s += emb[c];
-      const float mean = wave_sum(s) / (float)VD;
+      float sm = 0.f;
+      for (int c = lane; c < VD; c += 64) sm += emb[c];
+      const float mean = wave_sum(sm) / (float)VD;
       float ss = 0.f;
       for (int c = lane; c < VD; c += 64) {
         const float d = emb[c] - mean;
         ss += d * d;
       }
-      const float rstd = rsqrtf(wave_sum(ss) / (float)VD + 1e-5f);
-      for (int c = lane; c < VD; c += 64) {
-        float v = emb[c];
-        if (ln_scale > 0.f) v = (v - mean) * rstd * ln_scale;
-        if (in_weight > 0.f) v = v * in_weight;
-        emb[c] = v;
+      ss = wave_sum(ss);  // whole-wave reduction, outside the lane-0 branch
+      if (lane == 0) {
+        stat[0] = mean;
+        stat[1] = rsqrtf(ss / (float)VD + 1e-5f);
       }
     }
     __syncthreads();
+    const float mean = stat[0], rstd = stat[1];
+    for (int c = tid; c < VD; c += 256) {
+      float v = emb[c];
+      if (ln_scale > 0.f) v = (v - mean) * rstd * ln_scale;
+      if (in_weight > 0.f) v = v * in_weight;
+      emb[c] = v;
+    }
+    __syncthreads();
   }
-
-  // 4) mapper rows [chunk*HEAD_CHUNK, +HEAD_CHUNK)
-  const int o0 = chunk * HEAD_CHUNK;
-  for (int o = o0 + wave; o < o0 + HEAD_CHUNK && o < MO; o += 4) {
-    const float* w = mw + (long)o * VD;
-    float s = 0.f;
-    for (int c = lane; c < VD; c += 64) s += emb[c] * w[c];
-    s = wave_sum(s);
-    if (lane == 0) prefix[(long)b * MO + o] = s + mb[o];
+  // mapper: 16 outputs per wave in groups of 4, weight loads of a group in flight together
+  for (int g = 0; g < 4; ++g) {
+    const int ob = blockIdx.y * PREFIX_OUT + wave * 16 + g * 4;
+    if (ob >= MO) break;
+    float sacc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < VD; c0 += 256) {
+      float wv[4][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          wv[k][i] = mw[(long)min(ob + k, MO - 1) * VD + min(c0 + lane + 64 * i, VD - 1)];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = c0 + lane + 64 * i;
+          if (c < VD) sacc[k] += emb[c] * wv[k][i];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float v = wave_sum(sacc[k]);
+      if (lane == 0 && ob + k < MO) prefix[(long)b * MO + ob + k] = v + mb[ob + k];
+    }
   }
 }
 
+// x == nullptr: prefix only, from emb_in (vcap_prefix_project).  Otherwise the head writes emb
+// to enc_out (or emb_scratch when the caller does not want the encoder output) and the prefix
+// launch reads it from there.
 hipError_t vcap_vit_head_prefix_dispatch(const float* x, int B, int T, int N, int D, const float* ng, const float* nb,
                                          float neps, const float* pw, const float* pb, int VD, float ln_scale,
                                          float in_weight, const float* mw, const float* mb, int MO, float* enc_out,
-                                         float* prefix, const float* emb_in, hipStream_t s) {
-  if (D > 1024 || VD > 1024) return hipErrorInvalidValue;
-  const int chunks = prefix ? (MO + HEAD_CHUNK - 1) / HEAD_CHUNK : 1;
-  const dim3 grid(B, chunks), block(256);
-  hipLaunchKernelGGL(vcap_vit_head_prefix_kernel, grid, block, 0, s, x, T, N, D, ng, nb, neps, pw, pb, VD, ln_scale,
-                     in_weight, mw, mb, MO, enc_out, prefix, emb_in);
+                                         float* prefix, const float* emb_in, float* emb_scratch, hipStream_t s) {
+  if (D > 1024 || VD > 1024 || B <= 0) return hipErrorInvalidValue;
+  const float* emb = emb_in;
+  if (x) {
+    float* e = enc_out ? enc_out : emb_scratch;
+    if (!e) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(vcap_vit_head_kernel, dim3(B, (VD + HEAD_OUT - 1) / HEAD_OUT), dim3(256), 0, s, x, T, N, D, ng,
+                       nb, neps, pw, pb, VD, e);
+    if (hipError_t err = hipGetLastError()) return err;
+    emb = e;
+  }
+  if (!prefix) return hipSuccess;
+  if (!emb) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(vcap_prefix_map_kernel, dim3(B, (MO + PREFIX_OUT - 1) / PREFIX_OUT), dim3(256), 0, s, emb, VD,
+                     ln_scale, in_weight, mw, mb, MO, prefix);
   return hipGetLastError();
 }
 

@@ -11,23 +11,36 @@ from __future__ import annotations
 
 from typing import List, Optional, Sequence
 
+import ctypes as C
+
 import torch
 
+from . import _native as N
 from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder
 
 
 class CaptionPipeline:
     def __init__(self, encoder: HipViTEncoder, prefix: HipPrefix, decoder: HipGPT2Decoder, cfg: GenConfig,
-                 batch: int, prompt_ids: Sequence[int], device, depth: int = 2, gather=None):
+                 batch: int, prompt_ids: Sequence[int], device, depth: int = 2, gather=None,
+                 reserve_cus: int = 0):
         self.enc, self.pre, self.dec, self.cfg = encoder, prefix, decoder, cfg
         self.prompt_ids = list(prompt_ids)
         self.device = torch.device(device)
         self.depth = depth
         # The decode chain is latency-bound: give its stream the higher priority so its small
-        # workgroups are dispatched as soon as encode GEMM workgroups retire.
+        # workgroups are dispatched as soon as encode GEMM workgroups retire, and optionally keep
+        # the encode off `reserve_cus` CUs (a CU-masked stream) so the decode always finds some.
         lo, hi = torch.cuda.Stream.priority_range()
-        self.s_enc = torch.cuda.Stream(self.device, priority=lo)
-        self.s_dec = torch.cuda.Stream(self.device, priority=hi)
+        self._masked = None
+        with torch.cuda.device(self.device):
+            if reserve_cus > 0:
+                h = C.c_void_p()
+                N.check(N.lib().vcap_stream_create_cu_reserved(int(reserve_cus), C.byref(h)), "masked stream")
+                self._masked = h.value
+                self.s_enc = torch.cuda.ExternalStream(self._masked, device=self.device)
+            else:
+                self.s_enc = torch.cuda.Stream(self.device, priority=lo)
+            self.s_dec = torch.cuda.Stream(self.device, priority=hi)
         E = decoder.arch.n_embd
         self.prefix_bufs = [torch.empty(batch, prefix.prefix_len, E, device=self.device) for _ in range(depth)]
         self.ids_bufs = [torch.empty(batch, cfg.max_new_tokens, dtype=torch.int32, device=self.device)
@@ -72,3 +85,10 @@ class CaptionPipeline:
     def synchronize(self) -> None:
         self.s_enc.synchronize()
         self.s_dec.synchronize()
+
+    def close(self) -> None:
+        """Drain both streams and release the CU-masked encode stream (if one was created)."""
+        self.synchronize()
+        if self._masked is not None:
+            N.check(N.lib().vcap_stream_destroy(self._masked), "stream destroy")
+            self._masked = None

@@ -2,7 +2,7 @@
 // Replaces timm Attention with fused_attn=True -> F.scaled_dot_product_attention
 // (src/models/video_encoder.py:112-121; no mask, no causal, scale head_dim^-0.5).
 //
-// One workgroup (4 waves) per (frame, head).  K and V of the head are staged once in LDS:
+// f32 parity path: one workgroup (4 waves) per (frame, head).  K and V of the head are staged in LDS:
 // K row-major [NP][64] with an XOR chunk swizzle (conflict-free ds_read_b128 fragment
 // reads), V transposed to Vt[64][NP+pad].  Each wave owns 16-query tiles and computes
 // S^T = K Q^T on MFMA so a lane ends up holding 4 consecutive keys of ONE query per key
@@ -153,6 +153,168 @@ __global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __rest
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// bf16 path (the benchmark dtype).  Same S^T = K Q^T formulation and exact in-register softmax,
+// but nothing passes through VGPRs on the way to LDS and nothing is transposed by stores:
+//  * K and V rows arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB = 8 rows per wave
+//    instruction) into [key][64] images with the 16-byte-chunk XOR swizzle slot = c ^ (key & 7)
+//    applied on the source address;
+//  * the PV MFMA's Vt operand is read straight from the row-major V image with the gfx950
+//    transpose read ds_read_b64_tr_b16 (16-lane group: 4 keys x 16 dims -> lane i gets dim i);
+//    with the swizzle above the 8 keys a 32-lane half touches land on 64 distinct banks;
+//  * Q fragments of all of a wave's query tiles are loaded before the K/V wait;
+//  * softmax: exp2 with (1/sqrt(64)) * log2(e) folded into one FMA, P packed to bf16 with
+//    v_cvt_pk_bf16_f32.
+VCAP_DEV void glds16_attn(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+VCAP_DEV uint32_t cvt_pk_bf16(float lo, float hi) {
+  uint32_t r;
+  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+VCAP_DEV u32x2 tr_read(const char* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+  return __builtin_bit_cast(u32x2, v);
+}
+
+// One workgroup per (frame, head) pair; two of them share a CU (56 KiB of LDS, <= 128 VGPRs
+// for 4 waves per SIMD), so one pair's DMA overlaps the other's MFMA / softmax.  (A persistent
+// double-buffered variant measured slower: its doubled Q registers cost half the occupancy.)
+template <int KT, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(const bf16_t* __restrict__ qkv,
+                                                                             bf16_t* __restrict__ out, int N,
+                                                                             int H) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NP = KT * 16;
+  constexpr int QT_MAX = (KT + WAVES - 1) / WAVES;  // query tiles per wave (N <= NP)
+  static_assert(KT % 2 == 0, "PV consumes 32-key chunks");
+  char* Ks = smem;
+  char* Vs = smem + NP * 128;
+
+  const int bh = blockIdx.x;
+  const int bt = bh / H, h = bh - bt * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16_t* base = qkv + (long)bt * N * ld + h * 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+
+  // ---- K, V -> LDS by DMA (rows past N re-read row N-1: finite, masked out of the softmax)
+  for (int blk = wave; blk < NP / 8; blk += WAVES) {
+    const int r = blk * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    const bf16_t* src = base + (long)min(r, N - 1) * ld + c * 8;
+    glds16_attn(src + D, Ks + blk * 1024);
+    glds16_attn(src + 2 * D, Vs + blk * 1024);
+  }
+  // ---- this wave's Q fragments
+  const int qtiles = (N + 15) / 16;
+  u32x4 qf[QT_MAX][2];
+#pragma unroll
+  for (int i = 0; i < QT_MAX; ++i) {
+    const int q = min((wave + i * WAVES) * 16 + fr, N - 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) qf[i][s] = *reinterpret_cast<const u32x4*>(base + (long)q * ld + s * 32 + fg * 8);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const float c2 = 0.125f * 1.4426950408889634f;  // 64^-0.5 * log2(e)
+#pragma unroll
+  for (int i = 0; i < QT_MAX; ++i) {
+    const int qt = wave + i * WAVES;
+    if (qt >= qtiles) break;
+    // S^T[key][q] = K . Q^T
+    f32x4 st[KT];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const int key = kt * 16 + fr;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const u32x4 kf = *reinterpret_cast<const u32x4*>(Ks + key * 128 + (((s * 4 + fg) ^ (key & 7)) << 4));
+        acc = mfma_frag(kf, qf[i][s], acc, (bf16_t*)nullptr);
+      }
+      st[kt] = acc;  // keys kt*16 + 4*fg + r, query fr
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      if (kt * 16 + 16 > N) {  // wave-uniform: only the tail tiles hold padded keys
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kt * 16 + fg * 4 + r >= N) st[kt][r] = -INFINITY;
+      }
+      mx = fmaxf(mx, fmaxf(fmaxf(st[kt][0], st[kt][1]), fmaxf(st[kt][2], st[kt][3])));
+    }
+    mx = rows_max(mx);
+    const float mxc = mx * c2;
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(st[kt][r], c2, -mxc));
+        st[kt][r] = p;
+        sum += p;
+      }
+    sum = rows_sum(sum);
+
+    // O^T[d][q] = sum_key V[key][d] P^T[key][q]; k element j of lane group g <-> key
+    // 32c + 4g + j (j < 4) / 32c + 16 + 4g + (j - 4), matching the P^T fragment below
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int qr = fr >> 2, p4 = fr & 3;
+#pragma unroll
+    for (int c = 0; c < KT / 2; ++c) {
+      const u32x4 pf = (u32x4){cvt_pk_bf16(st[2 * c][0], st[2 * c][1]), cvt_pk_bf16(st[2 * c][2], st[2 * c][3]),
+                               cvt_pk_bf16(st[2 * c + 1][0], st[2 * c + 1][1]),
+                               cvt_pk_bf16(st[2 * c + 1][2], st[2 * c + 1][3])};
+      const int r0 = 32 * c + 4 * fg + qr, r1 = r0 + 16;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int ch = 2 * dt + (p4 >> 1);
+        const u32x2 lo = tr_read(Vs + r0 * 128 + ((ch ^ (r0 & 7)) << 4) + 8 * (p4 & 1));
+        const u32x2 hi = tr_read(Vs + r1 * 128 + ((ch ^ (r1 & 7)) << 4) + 8 * (p4 & 1));
+        o[dt] = mfma_frag((u32x4){lo.x, lo.y, hi.x, hi.y}, pf, o[dt], (bf16_t*)nullptr);
+      }
+    }
+    const int q = qt * 16 + fr;
+    if (q < N) {
+      const float inv = 1.0f / sum;
+      bf16_t* orow = out + ((long)bt * N + q) * D + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const f32x4 v = o[dt] * inv;  // O[q][d = dt*16 + 4*fg + r]
+        *reinterpret_cast<u32x2*>(orow + dt * 16 + 4 * fg) = (u32x2){cvt_pk_bf16(v.x, v.y), cvt_pk_bf16(v.z, v.w)};
+      }
+    }
+  }
+}
+
+template <int KT, int WAVES>
+static hipError_t launch_attn_bf16(const void* qkv, void* out, int BT, int N, int H, hipStream_t s) {
+  const size_t lds = (size_t)KT * 16 * 128 * 2;
+  static bool configured = false;
+  if (!configured) {
+    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_bf16_kernel<KT, WAVES>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    configured = true;
+  }
+  hipLaunchKernelGGL((vcap_vit_attention_bf16_kernel<KT, WAVES>), dim3(BT * H), dim3(WAVES * 64), lds, s,
+                     (const bf16_t*)qkv, (bf16_t*)out, N, H);
+  return hipGetLastError();
+}
+
 template <typename T, int KT>
 static hipError_t launch_attn(const void* qkv, void* out, int BT, int N, int H, hipStream_t s) {
   constexpr int NP = KT * 16;
@@ -175,9 +337,9 @@ hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int B
   const int kt = ((N + 31) / 32) * 2;  // keys padded to a multiple of 32
   if (dt == VCAP_DT_BF16) {
     switch (kt) {
-      case 2: return launch_attn<bf16_t, 2>(qkv, out, BT, N, H, s);
-      case 14: return launch_attn<bf16_t, 14>(qkv, out, BT, N, H, s);
-      case 18: return launch_attn<bf16_t, 18>(qkv, out, BT, N, H, s);
+      case 2: return launch_attn_bf16<2, 4>(qkv, out, BT, N, H, s);
+      case 14: return launch_attn_bf16<14, 8>(qkv, out, BT, N, H, s);
+      case 18: return launch_attn_bf16<18, 8>(qkv, out, BT, N, H, s);
       default: return hipErrorInvalidValue;
     }
   }

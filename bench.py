@@ -52,6 +52,8 @@ def parse():
                     help="no encode/decode overlap (each step's decode finishes before the next encode starts)")
     ap.add_argument("--reserve-cus", type=int, default=0,
                     help="CUs the encode stream leaves to the decode stream (CU-masked stream; 0 = none)")
+    ap.add_argument("--decode-blocks", type=int, default=0,
+                    help="cap the decode GEMV grids near this many workgroups (0 = whole-chip grids)")
     ap.add_argument("--cpu-baseline-s", type=float, default=20.0, help="CPU oracle time budget (0 disables)")
     return ap.parse_args()
 
@@ -112,6 +114,7 @@ def main():
         cfg = GenConfig(args.max_new, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, not args.no_graph)
     else:
         cfg = GenConfig.raw_greedy(args.max_new, ga.eos_token_id, not args.no_graph)
+    cfg.max_blocks = 0 if args.serial else args.decode_blocks
     gather = (lambda ids: gather_ids(ids, world)) if world > 1 else None
     pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev, gather=gather,
                            reserve_cus=0 if args.serial else args.reserve_cus)
@@ -180,6 +183,7 @@ def main():
                        "vit": args.vit, "gpt2": args.gpt2, "batch_per_gpu": B, "global_batch": world * B,
                        "frames": T, "max_new_tokens": args.max_new, "decode": args.decode,
                        "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}",
+                       "decode_block_cap": cfg.max_blocks,
                        "schedule": "serial" if args.serial else
                        f"encode(k+1) overlapped with decode(k) on 2 HIP streams (encode CU-masked off "
                        f"{args.reserve_cus} CUs)"},

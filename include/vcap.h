@@ -104,6 +104,9 @@ typedef struct vcap_gen_params {
   float repetition_penalty;  /* 1.0 disables */
   int eos_token_id, pad_token_id;
   int use_graph;             /* capture the whole decode into a hipGraph and replay it */
+  int max_blocks;            /* 0: whole-chip grids; > 0: cap the projection GEMV grids near this
+                                many workgroups (wider tiles per workgroup) - for a decode that
+                                shares the GPU with an encode holding most CUs */
 } vcap_gen_params;
 
 const char* vcap_last_error(void);

@@ -53,6 +53,20 @@ def test_greedy_fp32_token_identical(device, name):
 
 
 @pytest.mark.parametrize("name", ["tiny", "b16_b8"])
+@pytest.mark.parametrize("max_blocks", [40, 20])
+def test_greedy_fp32_capped_grids_token_identical(device, name, max_blocks):
+    """Decode GEMVs with 2 / 4 column tiles per workgroup (vcap_gen_params.max_blocks, the
+    setting used when the decode shares the GPU with an encode) give the same captions."""
+    meta, g, va, ga, enc, pre, dec, video = _models(name, "fp32", device)
+    _, prefix = enc.encode(video, pre)
+    prompt = meta["prompt_ids"] if len(meta["prompt_ids"]) else [ga.bos_token_id]
+    cfg = _hf_cfg(ga)
+    cfg.max_blocks = max_blocks
+    got = trim_generated(dec.generate_ids(prefix, prompt, cfg), ga.eos_token_id)
+    assert np.array_equal(np.array(got, dtype=np.int32), g["hf_greedy_ids"])
+
+
+@pytest.mark.parametrize("name", ["tiny", "b16_b8"])
 def test_raw_greedy_fp32_token_identical(device, name):
     meta, g, va, ga, enc, pre, dec, video = _models(name, "fp32", device)
     _, prefix = enc.encode(video, pre)

@@ -47,14 +47,15 @@ def run(name, reps):
                               0, 0, 0, 0, s), name)
 
 
-times = {(nm, p): [] for nm in shapes for p in (1, 2)}
-for p in (1, 2):
+POL = (1, 2, 0)
+times = {(nm, p): [] for nm in shapes for p in POL}
+for p in POL:
     lib.vcap_set_gemm_policy(p)
     for nm in shapes:
         run(nm, 3)
 torch.cuda.synchronize()
 for rnd_i in range(5):
-    for p in (1, 2):
+    for p in POL:
         lib.vcap_set_gemm_policy(p)
         for nm in shapes:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -67,7 +68,7 @@ lib.vcap_set_gemm_policy(0)
 for nm, (n, k, *_) in shapes.items():
     fl = 2.0 * M * n * k
     row = [f"{nm:5s} M={M} N={n} K={k}:"]
-    for p in (1, 2):
+    for p in POL:
         ms = statistics.median(times[(nm, p)])
-        row.append(f"tile{128 if p == 1 else 256} {ms * 1e3:7.1f} us {fl / ms / 1e9:7.1f} TF")
+        row.append(f"{['auto', 'tile128', 'tile256'][p]} {ms * 1e3:7.1f} us {fl / ms / 1e9:7.1f} TF")
     print("  ".join(row), flush=True)

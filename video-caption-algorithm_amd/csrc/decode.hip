@@ -750,7 +750,14 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
   return launch_generic<T, MT, NTB, PRO, EPI>(a, s);
 }
 
-static int rows_ntb(int epi) { return epi == EPI_LOGITS ? 4 : 1; }
+// 16-column tiles per workgroup: the lm_head always takes 4 (argmax partials per 64 columns);
+// the projections take 1 unless a grid cap asks for wider workgroups (2 or 4 tiles).
+static int rows_ntb(int epi, int N = 0, int max_blocks = 0) {
+  if (epi == EPI_LOGITS) return 4;
+  const int tiles = (N + 15) / 16;
+  if (max_blocks <= 0 || tiles <= max_blocks) return 1;
+  return tiles <= 2 * max_blocks ? 2 : 4;
+}
 
 int vcap_logit_blocks(int V, int M) {
   (void)M;
@@ -764,15 +771,19 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
   if (a.K % ks4 != 0 || a.M <= 0 || a.K <= 0 || a.N <= 0) return hipErrorInvalidValue;
   if (pro == PRO_LN && a.K > 1024) return hipErrorInvalidValue;
   if (epi == EPI_LOGITS && a.hist_ld > 64) return hipErrorInvalidValue;
-  const int ntb = rows_ntb(epi);
+  const int ntb = rows_ntb(epi, a.N, a.max_blocks);
   if (nblk_out) *nblk_out = (a.N + ntb * 16 - 1) / (ntb * 16);
   const bool one = a.M <= 16;
 #define VCAP_ROWS(TT, PP, EE, NT) \
   return one ? launch_rows<TT, 1, NT, PP, EE>(a, s) : launch_rows<TT, 2, NT, PP, EE>(a, s);
-#define VCAP_ROWS_EPI(TT)                                                                     \
-  if (pro == PRO_LN && epi == EPI_QKV) { VCAP_ROWS(TT, PRO_LN, EPI_QKV, 1) }                 \
-  if (pro == PRO_LN && epi == EPI_GELU) { VCAP_ROWS(TT, PRO_LN, EPI_GELU, 1) }               \
-  if (pro == PRO_DIRECT && epi == EPI_RESID) { VCAP_ROWS(TT, PRO_DIRECT, EPI_RESID, 1) }     \
+#define VCAP_ROWS_NT(TT, PP, EE)            \
+  if (ntb == 4) { VCAP_ROWS(TT, PP, EE, 4) } \
+  if (ntb == 2) { VCAP_ROWS(TT, PP, EE, 2) } \
+  VCAP_ROWS(TT, PP, EE, 1)
+#define VCAP_ROWS_EPI(TT)                                                                    \
+  if (pro == PRO_LN && epi == EPI_QKV) { VCAP_ROWS_NT(TT, PRO_LN, EPI_QKV) }                \
+  if (pro == PRO_LN && epi == EPI_GELU) { VCAP_ROWS_NT(TT, PRO_LN, EPI_GELU) }              \
+  if (pro == PRO_DIRECT && epi == EPI_RESID) { VCAP_ROWS_NT(TT, PRO_DIRECT, EPI_RESID) }    \
   if (pro == PRO_LN && epi == EPI_LOGITS) { VCAP_ROWS(TT, PRO_LN, EPI_LOGITS, 4) }
   if (dt == VCAP_DT_BF16) {
     VCAP_ROWS_EPI(bf16_t)
@@ -780,6 +791,7 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
     VCAP_ROWS_EPI(float)
   }
 #undef VCAP_ROWS_EPI
+#undef VCAP_ROWS_NT
 #undef VCAP_ROWS
   return hipErrorInvalidValue;
 }

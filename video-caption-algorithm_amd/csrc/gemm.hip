@@ -177,10 +177,34 @@ void vcap_gemm_set_policy(int p) { g_gemm_policy = p; }
 hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
                               long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s) {
   if (g_gemm_policy != 1 && vcap_gemm256_ok(in_dt, out_dt, lda, ldw, ldc, M, N, K, epi)) {
-    // 256x256 tiles need enough of them to fill the chip (one workgroup per CU)
-    const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-    if (g_gemm_policy == 2 || tiles256 >= 512)
+    // 256x256 tiles run one workgroup per CU: they need enough tiles to fill the chip, and a
+    // last round that is mostly empty costs a whole tile time.  Rows of the full rounds go to
+    // the 256x256 kernel, a small remainder to the 128x128 kernel (2 per CU, one short round).
+    const int tn = (N + 255) / 256;
+    const long tiles256 = (long)((M + 255) / 256) * tn;
+    if (g_gemm_policy == 2) return vcap_gemm256_dispatch(in_dt, out_dt, A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+    const int ncu = 256;
+    if (tiles256 >= ncu) {
+      const long rounds = tiles256 / ncu;
+      const long rem = tiles256 - rounds * ncu;
+      const bool plain = epi.G == 0 && (epi.res_mode == 0 || epi.res == (const float*)C);
+      const int m_full = (int)((rounds * ncu / tn) * 256);  // rows covered by whole 256-tile rounds
+      if (plain && rem > 0 && rem * 4 < ncu && m_full > 0 && m_full < M) {
+        if (hipError_t e = vcap_gemm256_dispatch(in_dt, out_dt, A, lda, W, ldw, C, ldc, m_full, N, K, epi, s))
+          return e;
+        const size_t ein = in_dt == VCAP_DT_BF16 ? 2 : 4, eout = out_dt == VCAP_DT_BF16 ? 2 : 4;
+        GemmEpi e2 = epi;
+        if (epi.res) e2.res = epi.res + (long)m_full * epi.ldr;
+        const void* A2 = (const char*)A + (size_t)m_full * lda * ein;
+        void* C2 = (char*)C + (size_t)m_full * ldc * eout;
+        if (in_dt == VCAP_DT_BF16 && out_dt == VCAP_DT_BF16)
+          return launch_gemm<bf16_t, bf16_t>(A2, lda, W, ldw, C2, ldc, M - m_full, N, K, e2, s);
+        if (in_dt == VCAP_DT_BF16 && out_dt == VCAP_DT_F32)
+          return launch_gemm<bf16_t, float>(A2, lda, W, ldw, C2, ldc, M - m_full, N, K, e2, s);
+        return launch_gemm<float, float>(A2, lda, W, ldw, C2, ldc, M - m_full, N, K, e2, s);
+      }
       return vcap_gemm256_dispatch(in_dt, out_dt, A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+    }
   }
   if (in_dt == VCAP_DT_BF16 && out_dt == VCAP_DT_BF16)
     return launch_gemm<bf16_t, bf16_t>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);

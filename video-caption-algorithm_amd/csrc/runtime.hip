@@ -190,7 +190,7 @@ int check_gpt2_launch(const vcap_gpt2_desc* d) {
 }
 
 int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_elems, int M, int S_new, int past,
-               hipStream_t s) {
+               int max_blocks, hipStream_t s) {
   const int E = d->n_embd, H = d->n_head, L = d->n_layer;
   const int dt = d->dtype;
   const size_t es = esize(dt);
@@ -206,7 +206,7 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     a.q_out = w.q;
     a.kc = (char*)w.kc + (size_t)l * page_elems * es;
     a.vc = (char*)w.vc + (size_t)l * page_elems * es;
-    a.page_table = w.pt; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past;
+    a.page_table = w.pt; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past; a.max_blocks = max_blocks;
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
     // 2) causal attention over the paged cache
     VCAP_TRY(vcap_decode_attention_dispatch(dt, w.q, a.kc, a.vc, w.pt, maxp, w.attn, M, H, S_new, past, s),
@@ -215,19 +215,19 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     RowsGemmArgs b;
     memset(&b, 0, sizeof(b));
     b.M = M; b.x = w.attn; b.ldx = E; b.w = ly.aproj_w; b.bias = ly.aproj_b; b.N = E; b.K = E;
-    b.out = w.h; b.ldo = E;
+    b.out = w.h; b.ldo = E; b.max_blocks = max_blocks;
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, b, nullptr, s), "attn_c_proj");
     // 4) ln_2 + c_fc + gelu_new
     RowsGemmArgs c;
     memset(&c, 0, sizeof(c));
     c.M = M; c.x = w.h; c.ldx = E; c.ln_g = ly.ln2_g; c.ln_b = ly.ln2_b; c.ln_eps = d->ln_eps;
-    c.w = ly.fc_w; c.bias = ly.fc_b; c.N = 4 * E; c.K = E; c.out = w.act; c.ldo = 4 * E;
+    c.w = ly.fc_w; c.bias = ly.fc_b; c.N = 4 * E; c.K = E; c.out = w.act; c.ldo = 4 * E; c.max_blocks = max_blocks;
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_GELU, c, nullptr, s), "c_fc");
     // 5) mlp c_proj + residual
     RowsGemmArgs e;
     memset(&e, 0, sizeof(e));
     e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.bias = ly.mproj_b; e.N = E;
-    e.K = 4 * E; e.out = w.h; e.ldo = E;
+    e.K = 4 * E; e.out = w.h; e.ldo = E; e.max_blocks = max_blocks;
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, e, nullptr, s), "mlp_c_proj");
   }
   return 0;
@@ -263,7 +263,7 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
   for (int step = 0; step < max_new; ++step) {
     const int S_new = step == 0 ? S0 : 1;
     const int past = step == 0 ? 0 : S0 + step - 1;
-    if (int rc = run_layers(d, w, maxp, page_elems, B * S_new, S_new, past, s)) return rc;
+    if (int rc = run_layers(d, w, maxp, page_elems, B * S_new, S_new, past, gp->max_blocks, s)) return rc;
     int nblk = 0;
     if (int rc = run_lm_head(d, w, B, S_new, logits_out ? logits_out + (size_t)step * B * V : nullptr, max_new, step,
                              gp->repetition_penalty, gp->min_new_tokens, gp->eos_token_id, &nblk, s))
@@ -626,7 +626,7 @@ int vcap_gpt2_prefill(const vcap_gpt2_desc* d, const float* prefix, const int* p
   VCAP_TRY(vcap_prefill_embed_dispatch(d->dtype, prefix, d->prefix_len, prompt_ids, prompt_len, d->wte, d->wpe, w.h, B,
                                        d->n_embd, s),
            "prefill_embed");
-  if (int rc = run_layers(d, w, maxp, pe, B * S0, S0, 0, s)) return rc;
+  if (int rc = run_layers(d, w, maxp, pe, B * S0, S0, 0, 0, s)) return rc;
   int nblk;
   return run_lm_head(d, w, B, S0, logits_out, 1, 0, 1.0f, 0, -1, &nblk, s);
 }
@@ -642,7 +642,7 @@ int vcap_gpt2_step(const vcap_gpt2_desc* d, const int* tokens, int rows, int S0,
   if (int rc = step_setup(d, rows, S0, max_new_tokens, workspace, ws_bytes, &w, &maxp, &pe, &scratch)) return rc;
   hipStream_t s = (hipStream_t)stream;
   VCAP_TRY(vcap_embed_tokens_dispatch(d->dtype, tokens, rows, d->wte, d->wpe, w.h, d->n_embd, pos, s), "embed_tokens");
-  if (int rc = run_layers(d, w, maxp, pe, rows, 1, pos, s)) return rc;
+  if (int rc = run_layers(d, w, maxp, pe, rows, 1, pos, 0, s)) return rc;
   int nblk;
   return run_lm_head(d, w, rows, 1, logits_out, 1, 0, 1.0f, 0, -1, &nblk, s);
 }

@@ -43,6 +43,7 @@ struct RowsGemmArgs {
   const int* nbanned;
   float rep_penalty;
   int min_new, eos;
+  int max_blocks;  // 0: one 16-column tile per workgroup; > 0: widen tiles to stay near this grid
 };
 
 hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,

@@ -182,6 +182,7 @@ class GenConfig:
     eos_token_id: int = 50256
     pad_token_id: int = 50256
     use_graph: bool = True
+    max_blocks: int = 0      # >0: narrower decode grids (decode sharing the GPU with an encode)
 
     @classmethod
     def raw_greedy(cls, max_new_tokens: int = 24, eos: int = 50256, use_graph: bool = True) -> "GenConfig":
@@ -268,7 +269,8 @@ class HipGPT2Decoder:
         gp = N.GenParams(max_new_tokens=mx, min_new_tokens=int(cfg.min_new_tokens),
                          no_repeat_ngram_size=int(cfg.no_repeat_ngram_size),
                          repetition_penalty=float(cfg.repetition_penalty), eos_token_id=int(cfg.eos_token_id),
-                         pad_token_id=int(cfg.pad_token_id), use_graph=int(bool(cfg.use_graph)))
+                         pad_token_id=int(cfg.pad_token_id), use_graph=int(bool(cfg.use_graph)),
+                         max_blocks=int(cfg.max_blocks))
         arr = (C.c_int * max(len(ids), 1))(*ids)
         ws = self.ws.get(self.workspace_bytes(B, len(ids), mx))
         N.check(N.lib().vcap_gpt2_generate(C.byref(self.desc), C.byref(gp), prefix.data_ptr(), arr, len(ids), B,

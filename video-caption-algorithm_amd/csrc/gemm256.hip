@@ -15,13 +15,14 @@
 //        phase 1: read A-h0 + B-h0 -> quadrant (0,0)     phase 2: read B-h1 -> (0,1)
 //        phase 3: read A-h1        -> (1,1)              phase 4: (registers only) -> (1,0)
 //  * the two wave groups (wr = 0 / 1, one wave of each per SIMD) run staggered by one barrier:
-//    while one group issues its MFMAs the other issues its ds_reads and LDS-DMA.  With the
-//    stagger a half may be restaged only >= 2 phases after its last read, so the staging order
-//    over an iteration (K-tiles t, t+1; buffers even/odd) is
-//        p1 B-h1(t+1)  p2 A-h1(t+1)  p3 A-h0(t+2)  p4 B-h0(t+2) | vmcnt(4): t+1 landed
-//        p5 B-h1(t+2)  p6 A-h1(t+2)  p7 A-h0(t+3)  p8 B-h0(t+3) | vmcnt(4): t+2 landed
-//    (2 half-tiles in flight across every barrier); a staged buffer is read only in a phase
-//    after the counted wait and the barrier that follow it in both groups;
+//    while one group issues its MFMAs the other issues its ds_reads and LDS-DMA.  Each phase
+//    retires its ds_reads (lgkmcnt(0)) before its first barrier, so a half can be restaged in
+//    the phase right after its last read, and the staging order over an iteration (K-tiles t,
+//    t+1; buffers even/odd) keeps 3 half-tiles in flight across every barrier:
+//        p1 A-h1(t+1)  p2 A-h0(t+2)  p3 B-h0(t+2)  p4 B-h1(t+2) | vmcnt(6): t+1 landed
+//        p5 A-h1(t+2)  p6 A-h0(t+3)  p7 B-h0(t+3)  p8 B-h1(t+3) | vmcnt(6): t+2 landed
+//    a staged buffer is read only in a phase after the counted wait and the barrier that
+//    follow it in both groups;
 //  * the MFMA takes the weight fragment as its A operand, so each lane ends up holding 4
 //    consecutive output COLUMNS of one row: vectorised bias / residual / store epilogue.
 #include "vcap_common.h"
@@ -137,10 +138,13 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
         for (int j = 0; j < 2; ++j) c[i][j] = mfma_frag(bf[j][s], af[i][s], c[i][j], (TIn*)nullptr);
     __builtin_amdgcn_s_setprio(0);
   };
+  // The phase's ds_reads are retired BEFORE its first barrier: once any wave is past that
+  // barrier, every wave's reads of the phase are done, so a half may be restaged in the very
+  // next phase even with the two wave groups staggered by a barrier.
   auto sync_reads = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     lds_fence();
     __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
   auto end_phase = [&]() {
     lds_fence();
@@ -149,14 +153,15 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
   };
 
   const int nk = K / BK;  // even, >= 2 (dispatcher)
-  // prologue: K-tile 0 complete; K-tile 1's A-h0, B-h0 in flight
+  // prologue: K-tile 0 complete; K-tile 1 minus its A-h1 in flight
   stA(0, 0);
+  stA(1, 0);
   stB(0, 0);
   stB(1, 0);
-  stA(1, 0);
   stA(0, 1);
   stB(0, 1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  stB(1, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   end_phase();
   // Stagger: the wr == 1 wave group runs one barrier behind, so on every SIMD one wave issues
   // its MFMAs while the other issues ds_reads / LDS-DMA.  (Balanced by wr == 0 after the loop.)
@@ -167,26 +172,26 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
     // ---- K-tile t (even buffer)
     rdB(b0, 0, t);
     rdA(a0, 0, t);
-    stB(1, t + 1);
+    stA(1, t + 1);
     sync_reads();
     mma(acc[0][0], a0, b0);
     end_phase();
 
     rdB(b1, 1, t);
-    stA(1, t + 1);
+    if (more) stA(0, t + 2);
     sync_reads();
     mma(acc[0][1], a0, b1);
     end_phase();
 
     rdA(a1, 1, t);
-    if (more) stA(0, t + 2);
+    if (more) stB(0, t + 2);
     sync_reads();
     mma(acc[1][1], a1, b1);
     end_phase();
 
     if (more) {
-      stB(0, t + 2);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // K-tile t+1 landed (this wave's part)
+      stB(1, t + 2);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K-tile t+1 landed (this wave's part)
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -197,26 +202,26 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
     // ---- K-tile t+1 (odd buffer)
     rdB(b0, 0, t + 1);
     rdA(a0, 0, t + 1);
-    if (more) stB(1, t + 2);
+    if (more) stA(1, t + 2);
     sync_reads();
     mma(acc[0][0], a0, b0);
     end_phase();
 
     rdB(b1, 1, t + 1);
-    if (more) stA(1, t + 2);
+    if (more) stA(0, t + 3);
     sync_reads();
     mma(acc[0][1], a0, b1);
     end_phase();
 
     rdA(a1, 1, t + 1);
-    if (more) stA(0, t + 3);
+    if (more) stB(0, t + 3);
     sync_reads();
     mma(acc[1][1], a1, b1);
     end_phase();
 
     if (more) {
-      stB(0, t + 3);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // K-tile t+2 landed
+      stB(1, t + 3);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K-tile t+2 landed
     }
     sync_reads();
     mma(acc[1][0], a1, b0);

@@ -80,6 +80,20 @@ def cpu_baseline(sd, va, ga, frames_np, budget_s: float, max_new: int):
             "p50_latency_ms": p50 * 1e3, "tokens_first": [int(t) for t in ids[0][:4]]}
 
 
+def fc1_traffic(M: int, N: int, K: int):
+    """HBM bytes per fc1 launch from the committed rocprofv3 PMC passes (profiles/), when they were
+    collected on this exact shape; None otherwise (PMC counters cannot be read inside bench.py)."""
+    p = ROOT / "profiles" / "r01_fc1_pmc_traffic.json"
+    try:
+        d = json.loads(p.read_text())
+    except (OSError, ValueError):
+        return None
+    if d.get("shape") != {"M": M, "N": N, "K": K}:
+        return None
+    b = d["per_launch_bytes"]
+    return float(b["fetch"] + b["write"])
+
+
 def main():
     args = parse()
     import numpy as np
@@ -190,9 +204,11 @@ def main():
             "p50_latency_ms": p50,
             "stage_ms_p50": {"vit_encode_prefix": statistics.median(vit_ms),
                              "prefix_ready_to_ids": statistics.median(dec_ms)},
-            "roofline": {"bound": "mfma", "kernel": "vit.fc1 vcap_gemm_kernel<bf16,bf16,1>",
+            "roofline": {"bound": "mfma", "kernel": "vit.fc1 vcap_gemm256_kernel<bf16,bf16,1>",
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                         "traffic": None, "flops_per_launch": fc1_flops, "avg_launch_ms": fc1_avg_s * 1e3,
+                         "traffic": fc1_traffic(M, va.mlp, va.dim),
+                         "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "flops_per_launch": fc1_flops, "avg_launch_ms": fc1_avg_s * 1e3,
                          "launches": fc1_n.value},
             "attention": {"kernel": "vit.attention", "avg_launch_ms": attn_avg_s * 1e3,
                           "achieved_tflops": attn_flops / attn_avg_s / 1e12,

@@ -122,6 +122,7 @@ int vcap_set_gemm_policy(int policy);
  *      latency-bound chain on another stream (the decode graph) always finds free CUs while
  *      the MFMA-bound encode fills the rest.  Destroy with vcap_stream_destroy. ---- */
 int vcap_stream_create_cu_reserved(int reserve_cus, void** stream);
+int vcap_stream_create_cu_mask(const uint32_t* mask, int words, void** stream);  /* raw CU bit mask */
 int vcap_stream_destroy(void* stream);
 
 /* ---- op-level entry points ---- */

@@ -330,6 +330,14 @@ int vcap_stream_create_cu_reserved(int reserve_cus, void** stream) {
   return 0;
 }
 
+int vcap_stream_create_cu_mask(const uint32_t* mask, int words, void** stream) {
+  if (!stream || !mask || words <= 0) return fail(VCAP_E_ARG, "vcap_stream_create_cu_mask: bad arguments");
+  hipStream_t s = nullptr;
+  VCAP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask), "hipExtStreamCreateWithCUMask");
+  *stream = (void*)s;
+  return 0;
+}
+
 int vcap_stream_destroy(void* stream) {
   VCAP_TRY(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
   return 0;

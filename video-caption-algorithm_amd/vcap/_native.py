@@ -66,6 +66,7 @@ SIGNATURES = {
     "vcap_abi_version": (i32, []),
     "vcap_set_gemm_policy": (i32, [i32]),
     "vcap_stream_create_cu_reserved": (i32, [i32, C.POINTER(C.c_void_p)]),
+    "vcap_stream_create_cu_mask": (i32, [C.POINTER(C.c_uint32), i32, C.POINTER(C.c_void_p)]),
     "vcap_stream_destroy": (i32, [vp]),
     "vcap_linear_bias": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, vp]),
     "vcap_gemm": (i32, [i32, i32, vp, i64, vp, i64, vp, i64, i32, i32, i32, vp, i32, vp, i64, i32, i32, i32, i32,

@@ -129,3 +129,20 @@ def test_golden_fixtures_are_self_consistent():
         meta, g = golden(name)
         assert g["hf_greedy_ids"].shape[0] == meta["B"]
         assert meta["vit_vs_hf_vitmodel_maxabs"] < 1e-4  # restated timm ViT == transformers.ViTModel
+
+
+@pytest.mark.slow
+def test_oracle_matches_reference_l14_medium():
+    """BASELINE configs[3] shapes (ViT-L/14, 257 tokens, GPT-2-medium): the oracle's backbone on
+    2 of the 64 recorded frames (CLS rows) and its greedy decode from the recorded prefix."""
+    meta, g, va, ga, sd, frames = case("l14_medium")
+    assert weights_digest_ok(sd, meta)
+    with torch.no_grad():
+        f2 = torch.from_numpy(frames.reshape(-1, 3, va.image, va.image)[:2].copy())
+        cls = O.vit_forward_features(sd, va, f2)[:, 0, :]
+        np.testing.assert_allclose(cls.numpy(), g["cls_tokens"][:2], rtol=1e-4, atol=1e-4)
+        x = torch.from_numpy(g["inputs_embeds"].copy())
+        ids, lg = O.generate_greedy(sd, ga, x, return_logits=True)
+    assert np.array_equal(ids.numpy(), g["hf_greedy_ids"])
+    got = np.take_along_axis(lg[0].numpy(), g["hf_greedy_logits_s0_top_i"].astype(np.int64), 1)
+    assert np.abs(got - g["hf_greedy_logits_s0_top_v"]).max() < 1e-4

@@ -31,6 +31,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "captions/sec + p50 encode+decode latency, 16-frame ViT-B/16 → GPT-2-small, 1/2/4/8 GPU"
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5000.0    # dense block-scaled fp8 MFMA (2x bf16 per clock)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
@@ -43,7 +44,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=8, help="videos per GPU")
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--max-new", type=int, default=24)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp8"],
+                    help="fp8: MXFP8 ViT QKV/fc1/fc2 GEMMs (BASELINE configs[4]); the decoder stays bf16")
     ap.add_argument("--decode", default="hf_greedy", choices=["hf_greedy", "raw_greedy"])
     ap.add_argument("--vit", default="vit_base_patch16_224")
     ap.add_argument("--gpt2", default="gpt2")
@@ -123,7 +125,7 @@ def main():
 
     enc = HipViTEncoder(sd, va, args.precision, dev)
     pre = HipPrefix(sd, ga.n_embd, device=dev)
-    dec = HipGPT2Decoder(sd, ga, args.precision, dev)
+    dec = HipGPT2Decoder(sd, ga, "bf16" if args.precision == "fp8" else args.precision, dev)
     if args.decode == "hf_greedy":
         cfg = GenConfig(args.max_new, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, not args.no_graph)
     else:
@@ -179,7 +181,7 @@ def main():
         M = B * T * va.tokens
         fc1_flops = 2.0 * M * va.mlp * va.dim
         fc1_avg_s = fc1_total.value / max(fc1_n.value, 1) / 1e3
-        peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+        peak = {"bf16": PEAK_BF16_TFLOPS, "fp8": PEAK_FP8_TFLOPS}.get(args.precision, PEAK_F32_TFLOPS)
         achieved = fc1_flops / fc1_avg_s / 1e12
         attn_flops = 4.0 * B * T * va.heads * va.tokens * va.tokens * 64
         attn_avg_s = at_total.value / max(at_n.value, 1) / 1e3
@@ -189,7 +191,7 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "captions/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.precision == "bf16" else "f32",
+            "scaling": "weak", "vs_baseline": None, "dtype": {"bf16": "bf16", "fp8": "mxfp8-e4m3 (ViT QKV/fc1/fc2) + bf16"}.get(args.precision, "f32"),
             "data": "synthetic (seeded U[0,1) frames, ImageNet-normalised; seeded random-init weights)",
             "config": {"workload": f"batch={B} synthetic {T}x3x224x224 videos per GPU, {args.vit} + {args.gpt2}, "
                                    f"{args.decode} decode max_new {args.max_new} (BASELINE configs[1]"
@@ -204,9 +206,12 @@ def main():
             "p50_latency_ms": p50,
             "stage_ms_p50": {"vit_encode_prefix": statistics.median(vit_ms),
                              "prefix_ready_to_ids": statistics.median(dec_ms)},
-            "roofline": {"bound": "mfma", "kernel": "vit.fc1 vcap_gemm256_kernel<bf16,bf16,1>",
+            "roofline": {"bound": "mfma",
+                         "kernel": {"bf16": "vit.fc1 vcap_gemm256_kernel<bf16,bf16,1>",
+                                    "fp8": "vit.fc1 vcap_gemm256_kernel<mxfp8,mxfp8,4>"}.get(
+                                        args.precision, "vit.fc1 vcap_gemm_kernel<f32,f32,1>"),
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                         "traffic": fc1_traffic(M, va.mlp, va.dim),
+                         "traffic": fc1_traffic(M, va.mlp, va.dim) if args.precision == "bf16" else None,
                          "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "flops_per_launch": fc1_flops, "avg_launch_ms": fc1_avg_s * 1e3,
                          "launches": fc1_n.value},

@@ -15,7 +15,7 @@
  *                           vit_fused_pool_temporal :127-186
  *   vcap_prefix_project     core/operators/normalization.py:6-13 apply_prefix_norm + the decoder
  *                           mapper (src/models/text_decoder.py:249), i.e. core/engine.py:44-50 -> :60-74
- *   vcap_gemm / vcap_layernorm / vcap_vit_attention
+ *   vcap_gemm / vcap_layernorm / vcap_vit_attention / vcap_gemm_mx / vcap_layernorm_mx
  *                           the timm ViT block arithmetic the reference drives through
  *                           src/models/video_encoder.py:112-174 (fused SDPA, tanh-GELU MLP,
  *                           in-place residual) - op-level entry points for the plugin registry
@@ -37,9 +37,15 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 2
+#define VCAP_ABI_VERSION 3
 
-enum { VCAP_DT_F32 = 0, VCAP_DT_BF16 = 1 };
+/* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
+ * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
+ * staging order: per (128-wide K-tile, group of 256 rows) one 1 KiB block laid out
+ * [k-block 0..3][row % 16][row / 16] - byte offset
+ *   ((k/128 * ceil(rows/256) + row/256) * 4 + (k%128)/32) * 256 + (row%16) * 16 + (row%256)/16,
+ * size vcap_mx_scale_bytes(rows, K).  Element value = e4m3 * 2^(scale - 127). */
+enum { VCAP_DT_F32 = 0, VCAP_DT_BF16 = 1, VCAP_DT_MXFP8 = 2 };
 enum { VCAP_E_ARG = -1000, VCAP_E_WORKSPACE = -1001, VCAP_E_UNSUPPORTED = -1002 };
 
 typedef struct vcap_vit_layer {
@@ -49,10 +55,15 @@ typedef struct vcap_vit_layer {
   const float* ln2_g; const float* ln2_b;
   const void* fc1_w; const float* fc1_b;     /* [4D, D] */
   const void* fc2_w; const float* fc2_b;     /* [D, 4D] */
+  /* dtype VCAP_DT_MXFP8 only: qkv_w / fc1_w / fc2_w are e4m3 and these their E8M0 scales
+   * (vcap_mx_quantize); proj_w and the patch-embed weight stay bf16 */
+  const uint8_t* qkv_ws; const uint8_t* fc1_ws; const uint8_t* fc2_ws;
 } vcap_vit_layer;
 
 typedef struct vcap_vit_desc {
-  int dtype;                 /* operand dtype of the block GEMMs (VCAP_DT_*) */
+  int dtype;                 /* operand dtype of the block GEMMs (VCAP_DT_*; MXFP8: QKV / fc1 / fc2
+                                in MXFP8 with LayerNorm and GELU emitting MXFP8 operands, patch-embed,
+                                attention and attn-proj in bf16) */
   int dim, depth, heads, patch, image, mlp, video_dim;
   int kpad;                  /* patch K (3*p*p) padded to the GEMM K step */
   float ln_eps;              /* 1e-6 (timm) */
@@ -134,6 +145,21 @@ int vcap_gemm(int in_dtype, int out_dtype, const void* A, int64_t lda, const voi
 int vcap_layernorm(int out_dtype, const float* x, int64_t ldx, void* y, int64_t ldy, const float* gamma,
                    const float* beta, int rows, int dim, float eps, void* stream);
 int vcap_vit_attention(int dtype, const void* qkv, void* out, int frames, int tokens, int heads, void* stream);
+
+/* ---- MXFP8 (BASELINE configs[4]: fp8 MFMA path for the ViT GEMMs) ----
+ * vcap_mx_quantize: rows of f32 / bf16 [rows, K] (row stride ldx) -> e4m3 [rows, K] + scales.
+ * vcap_layernorm_mx: LayerNorm (f32 rows) fused with the quantisation of its output.
+ * vcap_gemm_mx: C = epi(A . W^T) with A [M, K], W [N, K] MXFP8 (contiguous rows, K % 256 == 0);
+ *   out_dtype BF16 / F32 (res != NULL: C += ..., in place, f32) or MXFP8 (act must be 1 = bias +
+ *   GELU-tanh, C e4m3 [M, N] + c_scales, N % 128 == 0). */
+size_t vcap_mx_scale_bytes(int rows, int K);
+int vcap_mx_quantize(int in_dtype, const void* x, int64_t ldx, int rows, int K, void* q, uint8_t* scales,
+                     void* stream);
+int vcap_layernorm_mx(const float* x, int64_t ldx, void* q, uint8_t* scales, const float* gamma, const float* beta,
+                      int rows, int dim, float eps, void* stream);
+int vcap_gemm_mx(const void* A, const uint8_t* a_scales, const void* W, const uint8_t* w_scales, int out_dtype,
+                 void* C, int64_t ldc, uint8_t* c_scales, int M, int N, int K, const float* bias, int act,
+                 const float* res, void* stream);
 int vcap_vit_pool_temporal(int dtype, const void* feat, void* out, int bsz, int timesteps, int tokens, int channels,
                            int pool_gap, void* stream);
 int vcap_prefix_project(const float* emb, int B, int video_dim, const vcap_prefix_desc* pd, float* prefix_out,

@@ -278,3 +278,52 @@ def caption_ids(sd, vit_arch, gpt_arch, video: Tensor, prompt_ids: Sequence[int]
         return generate_raw_greedy(sd, gpt_arch, x, **gen_kw)
     ids, _ = generate_greedy(sd, gpt_arch, x, **gen_kw)
     return ids
+
+
+# ----------------------------------------------------------------------------- MXFP8 (configs[4])
+# The reference has no fp8 path; BASELINE.json configs[4] asks for an fp8 MFMA path for the ViT
+# GEMMs.  The format restated here is the one libvcap_hip.so computes in (include/vcap.h
+# VCAP_DT_MXFP8): OCP MX (Microscaling Formats v1.0) MXFP8-E4M3 - blocks of 32 consecutive
+# K elements sharing one E8M0 scale - with the shared exponent floor(log2(amax)) - 7 (the spec's
+# recipe with emax 7 instead of 8, so no element saturates), elements rounded to nearest-even.
+
+def mx_scale_index(rows: int, K: int) -> np.ndarray:
+    """Byte offset of scale (row, 32-block) in the GEMM staging layout -> int64 [rows, K/32]."""
+    r = np.arange(rows)[:, None]
+    k = (np.arange(K // 32) * 32)[None, :]
+    groups = (rows + 255) // 256
+    return (((k // 128) * groups + r // 256) * 4 + (k % 128) // 32) * 256 + (r % 16) * 16 + (r % 256) // 16
+
+
+def mx_scale_bytes(rows: int, K: int) -> int:
+    return (K // 128) * ((rows + 255) // 256) * 1024
+
+
+def mx_quantize(x: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """f32 [rows, K] -> (e4m3 bytes [rows, K] uint8, E8M0 scales [rows, K/32] uint8)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    rows, K = x.shape
+    blk = x.reshape(rows, K // 32, 32)
+    amax = np.abs(blk).max(-1).astype(np.float32)
+    sb = np.maximum(((amax.view(np.uint32) >> 23) & 0xFF).astype(np.int32) - 7, 0)
+    inv = ((254 - sb).astype(np.uint32) << 23).view(np.float32)
+    q = torch.from_numpy(blk * inv[..., None]).to(torch.float8_e4m3fn).view(torch.uint8).numpy()
+    return q.reshape(rows, K), sb.astype(np.uint8)
+
+
+def mx_dequantize(q: np.ndarray, sb: np.ndarray) -> np.ndarray:
+    rows, K = q.shape
+    v = torch.from_numpy(np.ascontiguousarray(q)).view(torch.float8_e4m3fn).float().numpy().reshape(rows, K // 32, 32)
+    return (v * np.exp2(sb.astype(np.float32) - 127.0)[..., None]).reshape(rows, K)
+
+
+def mx_pack_scales(sb: np.ndarray) -> np.ndarray:
+    """[rows, K/32] scales -> the flat staging-layout array (vcap_mx_scale_bytes long)."""
+    rows, nb = sb.shape
+    out = np.zeros(mx_scale_bytes(rows, nb * 32), np.uint8)
+    out[mx_scale_index(rows, nb * 32)] = sb
+    return out
+
+
+def mx_unpack_scales(flat: np.ndarray, rows: int, K: int) -> np.ndarray:
+    return np.asarray(flat)[mx_scale_index(rows, K)]

@@ -146,3 +146,21 @@ def test_oracle_matches_reference_l14_medium():
     assert np.array_equal(ids.numpy(), g["hf_greedy_ids"])
     got = np.take_along_axis(lg[0].numpy(), g["hf_greedy_logits_s0_top_i"].astype(np.int64), 1)
     assert np.abs(got - g["hf_greedy_logits_s0_top_v"]).max() < 1e-4
+
+
+def test_oracle_mx_quantize_properties():
+    """MXFP8 restatement: round trip within half an e4m3 step, block max in [128, 256) after
+    scaling, zero block -> scale 0, layout round trip."""
+    g = np.random.default_rng(0)
+    x = (g.standard_normal((300, 512)) * np.exp2(g.integers(-20, 20, (300, 16, 1))).repeat(32, -1).reshape(300, 512))
+    x = x.astype(np.float32)
+    x[7, 64:96] = 0
+    q, s = O.mx_quantize(x)
+    d = O.mx_dequantize(q, s)
+    assert s[7, 2] == 0 and not d[7, 64:96].any()
+    half = np.repeat(np.exp2(s.astype(np.float64) - 127.0) * 8.0, 32, axis=1)
+    assert (np.abs(d - x) <= half).all()
+    top = np.abs(x).reshape(300, 16, 32).max(-1) * np.exp2(127.0 - s)
+    nz = s > 0
+    assert ((top[nz] >= 128) & (top[nz] < 256)).all()
+    assert np.array_equal(O.mx_unpack_scales(O.mx_pack_scales(s), 300, 512), s)

@@ -176,6 +176,10 @@ void vcap_gemm_set_policy(int p) { g_gemm_policy = p; }
 // in_dt: operand dtype; out_dt: C dtype (the residual stream is f32)
 hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
                               long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s) {
+  if (in_dt == VCAP_DT_MXFP8) {  // block-scaled fp8: the 256x256 kernel only
+    if (!vcap_gemm256_ok(in_dt, out_dt, lda, ldw, ldc, M, N, K, epi)) return hipErrorInvalidValue;
+    return vcap_gemm256_dispatch(in_dt, out_dt, A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  }
   if (g_gemm_policy != 1 && vcap_gemm256_ok(in_dt, out_dt, lda, ldw, ldc, M, N, K, epi)) {
     // 256x256 tiles run one workgroup per CU: they need enough tiles to fill the chip, and a
     // last round that is mostly empty costs a whole tile time.  Rows of the full rounds go to
@@ -215,4 +219,4 @@ hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, co
   return hipErrorInvalidValue;
 }
 
-int vcap_gemm_k_align(int in_dt) { return in_dt == VCAP_DT_BF16 ? 64 : 32; }
+int vcap_gemm_k_align(int in_dt) { return in_dt == VCAP_DT_MXFP8 ? 256 : in_dt == VCAP_DT_BF16 ? 64 : 32; }

@@ -34,6 +34,10 @@ constexpr int TM = 256, TN = 256, ROWB = 128;
 constexpr int HALF = 128 * ROWB;  // 16 KiB
 constexpr int BUF = 4 * HALF;     // one K-tile: A-h0 A-h1 B-h0 B-h1
 constexpr int LDS_BYTES = 2 * BUF;
+// MXFP8: 4 scale buffers (K-tile kt in buffer kt & 3), each = the A block then the W block
+// (1 KiB each, the global mx_scale_index layout of vcap_common.h)
+constexpr int SBUF = 2048;
+constexpr int LDS_BYTES_MX = LDS_BYTES + 4 * SBUF;
 
 VCAP_DEV void glds16(const void* g, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -58,6 +62,11 @@ VCAP_DEV void half_offsets(uint32_t (&off)[2], long ld, int rows, int base, int 
   }
 }
 
+VCAP_DEV void glds4(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 4, 0, 0);
+}
+
 VCAP_DEV void stage_half(const char* base_k, const uint32_t (&off)[2], char* lds_half, int wave) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) glds16(base_k + off[i], lds_half + (wave * 2 + i) * 1024);
@@ -77,6 +86,7 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
                                                            int M, int N, int K, GemmEpi epi) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BK = ROWB / sizeof(TIn);
+  constexpr bool MX = sizeof(TIn) == 1;  // MXFP8: one scaled 16x16x128 MFMA per K-tile and fragment
 
   const int tiles_n = (N + TN - 1) / TN;
   const int tiles_m = (M + TM - 1) / TM;
@@ -101,42 +111,103 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  u32x4 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+  // fragment pairs: lo = first 16-byte chunk, hi = second (MXFP8: one 8-register MFMA operand)
+  u32x8 a0[4], a1[4], b0[2], b1[2];
+  int sa[2], sb;  // MXFP8 scales of the current K-tile: A (byte X*4+i -> sa[X] byte i), W (byte Y*2+j)
 
   uint32_t offA[2][2], offB[2][2];
   half_offsets<TIn, 6>(offA[0], lda, M, m0, 0, wave, lane);
   half_offsets<TIn, 6>(offA[1], lda, M, m0, 1, wave, lane);
   half_offsets<TIn, 5>(offB[0], ldw, N, n0, 0, wave, lane);
   half_offsets<TIn, 5>(offB[1], ldw, N, n0, 1, wave, lane);
+  // MXFP8 scales of K-tile kt: waves 0-3 stage the A block of row group m0/256, waves 4-7 the W
+  // block of column group n0/256 (256 B per wave), with the A-h0 half of that K-tile.
+  const uint8_t* s_src = nullptr;  // wave-uniform; the lane adds lane * 4
+  long s_stride = 0;
+  if constexpr (MX) {
+    const int ga = (M + 255) >> 8, gw = (N + 255) >> 8;
+    s_src = wave < 4 ? epi.a_scale + (long)(m0 >> 8) * 1024 : epi.w_scale + (long)(n0 >> 8) * 1024;
+    s_src += (wave & 3) * 256;
+    s_stride = (long)(wave < 4 ? ga : gw) * 1024;
+  }
+  char* const sbase = smem + 2 * BUF;
   auto stA = [&](int X, int kt) {
     stage_half((const char*)A + (long)kt * ROWB, offA[X], smem + (kt & 1) * BUF + X * HALF, wave);
+    if constexpr (MX) {
+      if (X == 0) glds4(s_src + kt * s_stride + lane * 4, sbase + (kt & 3) * SBUF + wave * 256);
+    }
   };
   auto stB = [&](int Y, int kt) {
     stage_half((const char*)W + (long)kt * ROWB, offB[Y], smem + (kt & 1) * BUF + (2 + Y) * HALF, wave);
   };
-  auto rdA = [&](u32x4 (&f)[4][2], int X, int kt) {
+  // Lane group fg reads 16-byte chunks fg and 4 + fg of each row: bf16 / f32 feed them to the two
+  // K sub-steps; MXFP8 feeds both to one scaled MFMA, whose operand layout is exactly that
+  // (K [16 fg, +16) and [64 + 16 fg, +16), tools/mx_layout_probe.hip) while the scale of lane
+  // group b applies to K block [32 b, +32).
+  auto rdA = [&](u32x8 (&f)[4], int X, int kt) {
     const char* h = smem + (kt & 1) * BUF + X * HALF;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) f[i][s] = frag(h, wr * 64 + i * 16 + fr, s * 4 + fg);
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr * 64 + i * 16 + fr;
+      f[i] = cat8(frag(h, row, fg), frag(h, row, 4 + fg));
+    }
   };
-  auto rdB = [&](u32x4 (&f)[2][2], int Y, int kt) {
+  auto rdB = [&](u32x8 (&f)[2], int Y, int kt) {
     const char* h = smem + (kt & 1) * BUF + (2 + Y) * HALF;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) f[j][s] = frag(h, wc * 32 + j * 16 + fr, s * 4 + fg);
+    for (int j = 0; j < 2; ++j) {
+      const int row = wc * 32 + j * 16 + fr;
+      f[j] = cat8(frag(h, row, fg), frag(h, row, 4 + fg));
+    }
   };
-  auto mma = [&](f32x4 (&c)[4][2], const u32x4 (&af)[4][2], const u32x4 (&bf)[2][2]) {
+  // MXFP8: this lane's scales of K-tile kt - A rows wr*128 + X*64 + i*16 + fr (byte i of sa[X]),
+  // W rows wc*64 + Y*32 + j*16 + fr (byte Y*2 + j of sb), block fg
+  auto rdS = [&](int kt) {
+    if constexpr (MX) {
+      const char* sb_ = sbase + (kt & 3) * SBUF + fg * 256 + fr * 16;
+      const u32x2 a = *reinterpret_cast<const u32x2*>(sb_ + wr * 8);
+      sa[0] = (int)a.x;
+      sa[1] = (int)a.y;
+      sb = (int)*reinterpret_cast<const uint32_t*>(sb_ + 1024 + wc * 4);
+    }
+  };
+  auto mma = [&](f32x4 (&c)[4][2], const u32x8 (&af)[4], int X, const u32x8 (&bf)[2], int Y) {
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
+    if constexpr (MX) {
+      const int s_a = sa[X];
+      asm volatile("s_nop 1" ::: "memory");  // VALU -> MFMA operand wait states (asm MFMAs)
+      // OPSEL must be an immediate: expand (Y, i, j) explicitly
+#define VCAP_MX4(YY)                                           \
+      mfma_mx<YY * 2 + 0, 0>(bf[0], sb, af[0], s_a, c[0][0]);  \
+      mfma_mx<YY * 2 + 1, 0>(bf[1], sb, af[0], s_a, c[0][1]);  \
+      mfma_mx<YY * 2 + 0, 1>(bf[0], sb, af[1], s_a, c[1][0]);  \
+      mfma_mx<YY * 2 + 1, 1>(bf[1], sb, af[1], s_a, c[1][1]);  \
+      mfma_mx<YY * 2 + 0, 2>(bf[0], sb, af[2], s_a, c[2][0]);  \
+      mfma_mx<YY * 2 + 1, 2>(bf[1], sb, af[2], s_a, c[2][1]);  \
+      mfma_mx<YY * 2 + 0, 3>(bf[0], sb, af[3], s_a, c[3][0]);  \
+      mfma_mx<YY * 2 + 1, 3>(bf[1], sb, af[3], s_a, c[3][1]);
+      if (Y == 0) {
+        VCAP_MX4(0)
+      } else {
+        VCAP_MX4(1)
+      }
+#undef VCAP_MX4
+    } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) c[i][j] = mfma_frag(bf[j][s], af[i][s], c[i][j], (TIn*)nullptr);
+        for (int j = 0; j < 2; ++j) c[i][j] = mfma_frag(lo4(bf[j]), lo4(af[i]), c[i][j], (TIn*)nullptr);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) c[i][j] = mfma_frag(hi4(bf[j]), hi4(af[i]), c[i][j], (TIn*)nullptr);
+    }
     __builtin_amdgcn_s_setprio(0);
+  };
+  // counted waits: 2 LDS-DMA per thread per staged half, plus the scale row with each A-h0 (MX)
+  auto wait_landed = [&]() {
+    if constexpr (MX) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   };
   // The phase's ds_reads are retired BEFORE its first barrier: once any wave is past that
   // barrier, every wave's reads of the phase are done, so a half may be restaged in the very
@@ -161,7 +232,7 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
   stA(0, 1);
   stB(0, 1);
   stB(1, 1);
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  wait_landed();
   end_phase();
   // Stagger: the wr == 1 wave group runs one barrier behind, so on every SIMD one wave issues
   // its MFMAs while the other issues ds_reads / LDS-DMA.  (Balanced by wr == 0 after the loop.)
@@ -172,64 +243,111 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
     // ---- K-tile t (even buffer)
     rdB(b0, 0, t);
     rdA(a0, 0, t);
+    rdS(t);
     stA(1, t + 1);
     sync_reads();
-    mma(acc[0][0], a0, b0);
+    mma(acc[0][0], a0, 0, b0, 0);
     end_phase();
 
     rdB(b1, 1, t);
     if (more) stA(0, t + 2);
     sync_reads();
-    mma(acc[0][1], a0, b1);
+    mma(acc[0][1], a0, 0, b1, 1);
     end_phase();
 
     rdA(a1, 1, t);
     if (more) stB(0, t + 2);
     sync_reads();
-    mma(acc[1][1], a1, b1);
+    mma(acc[1][1], a1, 1, b1, 1);
     end_phase();
 
     if (more) {
       stB(1, t + 2);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K-tile t+1 landed (this wave's part)
+      wait_landed();  // K-tile t+1 landed (this wave's part)
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     sync_reads();
-    mma(acc[1][0], a1, b0);
+    mma(acc[1][0], a1, 1, b0, 0);
     end_phase();
 
     // ---- K-tile t+1 (odd buffer)
     rdB(b0, 0, t + 1);
     rdA(a0, 0, t + 1);
+    rdS(t + 1);
     if (more) stA(1, t + 2);
     sync_reads();
-    mma(acc[0][0], a0, b0);
+    mma(acc[0][0], a0, 0, b0, 0);
     end_phase();
 
     rdB(b1, 1, t + 1);
     if (more) stA(0, t + 3);
     sync_reads();
-    mma(acc[0][1], a0, b1);
+    mma(acc[0][1], a0, 0, b1, 1);
     end_phase();
 
     rdA(a1, 1, t + 1);
     if (more) stB(0, t + 3);
     sync_reads();
-    mma(acc[1][1], a1, b1);
+    mma(acc[1][1], a1, 1, b1, 1);
     end_phase();
 
     if (more) {
       stB(1, t + 3);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K-tile t+2 landed
+      wait_landed();  // K-tile t+2 landed
     }
     sync_reads();
-    mma(acc[1][0], a1, b0);
+    mma(acc[1][0], a1, 1, b0, 0);
     end_phase();
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();
+  if constexpr (MX) mfma_mx_drain();
 
   // ---- epilogue: lane holds C[m][n .. n+3] of each 16x16 tile (m = .. + fr, n = .. + 4*fg)
+  if constexpr (EPI == 4) {
+    // bias + GELU, re-quantised to MXFP8 for the next GEMM: the 32-column block
+    // n0 + wc*64 + qn*32 of row m lives in this lane (j = 0, 1) and the lanes fg = 0..3 of the
+    // same fr, so its max |x| is a 2-step permlane reduction.
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn) {
+        const int nb = n0 + wc * 64 + qn * 32;
+        f32x4 bias[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int n = min(nb + j * 16 + fg * 4, N - 4);
+          bias[j] = *reinterpret_cast<const f32x4*>(epi.bias + n);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wr * 128 + qm * 64 + i * 16 + fr;
+          f32x4 v[2];
+          float amax = 0.f;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            v[j] = acc[qm][qn][i][j] + bias[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[j][e] = gelu_tanh(v[j][e]);
+              amax = fmaxf(amax, fabsf(v[j][e]));
+            }
+          }
+          amax = rows_max(amax);
+          const int sbyte = mx_scale_byte(amax);
+          const float inv = mx_inv_scale(sbyte);
+          if (m < M && nb < N) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const f32x4 q = v[j] * inv;
+              *reinterpret_cast<uint32_t*>((uint8_t*)C + (long)m * ldc + nb + j * 16 + fg * 4) =
+                  pack_fp8x4(q.x, q.y, q.z, q.w);
+            }
+            if (fg == 0) epi.c_scale[mx_scale_index(m, nb, (M + 255) >> 8)] = (uint8_t)sbyte;
+          }
+        }
+      }
+  } else {
 #pragma unroll
   for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
@@ -266,20 +384,22 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
           }
         }
       }
+  }
 }
 
 template <typename TIn, typename TOut, int EPI>
 static hipError_t launch256_epi(const void* A, long lda, const void* W, long ldw, void* C, long ldc, int M, int N,
                                 int K, const GemmEpi& epi, hipStream_t s) {
+  constexpr int lds = sizeof(TIn) == 1 ? LDS_BYTES_MX : LDS_BYTES;
   static bool configured = false;
   if (!configured) {
     hipError_t e = hipFuncSetAttribute((const void*)vcap_gemm256_kernel<TIn, TOut, EPI>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     configured = true;
   }
   const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
-  hipLaunchKernelGGL((vcap_gemm256_kernel<TIn, TOut, EPI>), dim3(tiles), dim3(512), LDS_BYTES, s, (const TIn*)A, lda,
+  hipLaunchKernelGGL((vcap_gemm256_kernel<TIn, TOut, EPI>), dim3(tiles), dim3(512), lds, s, (const TIn*)A, lda,
                      (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, epi);
   return hipGetLastError();
 }
@@ -287,26 +407,34 @@ static hipError_t launch256_epi(const void* A, long lda, const void* W, long ldw
 template <typename TIn, typename TOut>
 static hipError_t launch256(const void* A, long lda, const void* W, long ldw, void* C, long ldc, int M, int N, int K,
                             const GemmEpi& epi, hipStream_t s) {
-  const bool plain_rows = epi.G == 0;
-  if (plain_rows && epi.res_mode == 0 && epi.act == 0)
-    return launch256_epi<TIn, TOut, 0>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
-  if constexpr (sizeof(TOut) == sizeof(TIn)) {
-    if (plain_rows && epi.res_mode == 0 && epi.act == 1)
-      return launch256_epi<TIn, TOut, 1>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if constexpr (sizeof(TOut) == 1) {
+    return launch256_epi<TIn, TOut, 4>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);  // MXFP8 out (bias + gelu)
+  } else {
+    const bool plain_rows = epi.G == 0;
+    if (plain_rows && epi.res_mode == 0 && epi.act == 0)
+      return launch256_epi<TIn, TOut, 0>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+    if constexpr (sizeof(TOut) == sizeof(TIn)) {
+      if (plain_rows && epi.res_mode == 0 && epi.act == 1)
+        return launch256_epi<TIn, TOut, 1>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+    }
+    if constexpr (sizeof(TOut) == 4) {
+      if (plain_rows && epi.res_mode == 1 && epi.act == 0 && epi.res == (const float*)C && epi.ldr == ldc)
+        return launch256_epi<TIn, TOut, 2>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+    }
+    return launch256_epi<TIn, TOut, 3>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
   }
-  if constexpr (sizeof(TOut) == 4) {
-    if (plain_rows && epi.res_mode == 1 && epi.act == 0 && epi.res == (const float*)C && epi.ldr == ldc)
-      return launch256_epi<TIn, TOut, 2>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
-  }
-  return launch256_epi<TIn, TOut, 3>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
 }
 
 // Shapes this kernel takes: K a multiple of two K-tiles, N and the strides in whole 16-byte
 // vectors for the epilogue, 16-byte aligned bias / residual rows.
 bool vcap_gemm256_ok(int in_dt, int out_dt, long lda, long ldw, long ldc, int M, int N, int K, const GemmEpi& epi) {
-  const int bk = in_dt == VCAP_DT_BF16 ? 64 : 32;
+  const int bk = in_dt == VCAP_DT_MXFP8 ? 128 : in_dt == VCAP_DT_BF16 ? 64 : 32;
   if (K % (2 * bk) != 0 || N % 16 != 0 || M <= 0) return false;
-  const int ein = in_dt == VCAP_DT_BF16 ? 8 : 4;
+  const int ein = in_dt == VCAP_DT_MXFP8 ? 16 : in_dt == VCAP_DT_BF16 ? 8 : 4;
+  if (in_dt == VCAP_DT_MXFP8 && (!epi.a_scale || !epi.w_scale)) return false;
+  if (out_dt == VCAP_DT_MXFP8 && (in_dt != VCAP_DT_MXFP8 || N % 128 || ldc % 16 || epi.act != 1 || !epi.bias ||
+                                  !epi.c_scale || epi.G || epi.res_mode))
+    return false;
   if (lda % ein || ldw % ein) return false;
   if (ldc % 4) return false;
   if (epi.bias && ((uintptr_t)epi.bias & 15)) return false;
@@ -323,5 +451,11 @@ hipError_t vcap_gemm256_dispatch(int in_dt, int out_dt, const void* A, long lda,
     return launch256<bf16_t, float>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
   if (in_dt == VCAP_DT_F32 && out_dt == VCAP_DT_F32)
     return launch256<float, float>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if (in_dt == VCAP_DT_MXFP8 && out_dt == VCAP_DT_BF16)
+    return launch256<fp8_t, bf16_t>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if (in_dt == VCAP_DT_MXFP8 && out_dt == VCAP_DT_F32)
+    return launch256<fp8_t, float>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if (in_dt == VCAP_DT_MXFP8 && out_dt == VCAP_DT_MXFP8)
+    return launch256<fp8_t, fp8_t>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
   return hipErrorInvalidValue;
 }

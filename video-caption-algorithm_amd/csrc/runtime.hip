@@ -38,7 +38,8 @@ int hip_fail(hipError_t e, const char* where) {
     if (_e != hipSuccess) return hip_fail(_e, where); \
   } while (0)
 
-size_t esize(int dt) { return dt == VCAP_DT_BF16 ? 2 : 4; }
+size_t esize(int dt) { return dt == VCAP_DT_MXFP8 ? 1 : dt == VCAP_DT_BF16 ? 2 : 4; }
+size_t mx_scale_bytes(int rows, int K) { return (size_t)(K / 128) * (size_t)((rows + 255) / 256) * 1024; }
 size_t al(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Carver {
@@ -95,31 +96,48 @@ struct VitBufs {
   void* qkv;
   void* attn;
   void* act;
+  uint8_t* xn_s;   // MXFP8 scales of xn / act
+  uint8_t* act_s;
 };
+
+// operand dtype of patch-embed / qkv output / attention / attn-proj: bf16 in the MXFP8 mode
+int vit_adt(int dt) { return dt == VCAP_DT_MXFP8 ? VCAP_DT_BF16 : dt; }
 
 VitBufs carve_vit(Carver& c, const vcap_vit_desc* d, int B, int T) {
   const int tokens = (d->image / d->patch) * (d->image / d->patch) + 1;
   const size_t M = (size_t)B * T * tokens;
-  const size_t es = esize(d->dtype);
+  const size_t es = esize(d->dtype), ea = esize(vit_adt(d->dtype));
   const size_t npatch = (size_t)B * T * (tokens - 1);
   VitBufs v;
   v.x = (float*)c.take(M * d->dim * 4);
   v.xn = c.take(M * d->dim * es);
-  v.qkv = c.take(M * 3 * d->dim * es);
-  v.attn = c.take(M * d->dim * es);
+  v.qkv = c.take(M * 3 * d->dim * ea);
+  v.attn = c.take(M * d->dim * ea);
   size_t act = M * d->mlp * es;
-  const size_t patches = npatch * d->kpad * es;
+  const size_t patches = npatch * d->kpad * ea;
   v.act = c.take(act > patches ? act : patches);
+  v.xn_s = v.act_s = nullptr;
+  if (d->dtype == VCAP_DT_MXFP8) {
+    v.xn_s = (uint8_t*)c.take(mx_scale_bytes((int)M, d->dim));
+    v.act_s = (uint8_t*)c.take(mx_scale_bytes((int)M, d->mlp));
+  }
   return v;
 }
 
 int check_vit(const vcap_vit_desc* d) {
   if (!d || !d->layers) return fail(VCAP_E_ARG, "vit desc is null");
-  if (d->dtype != VCAP_DT_F32 && d->dtype != VCAP_DT_BF16) return fail(VCAP_E_ARG, "vit dtype");
+  if (d->dtype != VCAP_DT_F32 && d->dtype != VCAP_DT_BF16 && d->dtype != VCAP_DT_MXFP8)
+    return fail(VCAP_E_ARG, "vit dtype");
   if (d->heads * 64 != d->dim) return fail(VCAP_E_UNSUPPORTED, "vit head_dim must be 64");
   const int ka = vcap_gemm_k_align(d->dtype);
-  if (d->dim % ka || d->mlp % ka || d->kpad % ka || d->kpad < 3 * d->patch * d->patch)
+  if (d->dim % ka || d->mlp % ka || d->kpad % vcap_gemm_k_align(vit_adt(d->dtype)) || d->kpad < 3 * d->patch * d->patch)
     return fail(VCAP_E_UNSUPPORTED, "vit dims must be multiples of the GEMM K step");
+  if (d->dtype == VCAP_DT_MXFP8) {
+    if (d->dim > 1024) return fail(VCAP_E_UNSUPPORTED, "MXFP8 LayerNorm holds rows of <= 1024 in registers");
+    for (int l = 0; l < d->depth; ++l)
+      if (!d->layers[l].qkv_ws || !d->layers[l].fc1_ws || !d->layers[l].fc2_ws)
+        return fail(VCAP_E_ARG, "MXFP8 vit layer without weight scales");
+  }
   if (d->image % d->patch) return fail(VCAP_E_ARG, "image not divisible by patch");
   const int tokens = (d->image / d->patch) * (d->image / d->patch) + 1;
   if (tokens > 288) return fail(VCAP_E_UNSUPPORTED, "more than 288 tokens");
@@ -380,6 +398,54 @@ int vcap_layernorm(int out_dtype, const float* x, int64_t ldx, void* y, int64_t 
   return 0;
 }
 
+size_t vcap_mx_scale_bytes(int rows, int K) {
+  if (rows <= 0 || K <= 0 || K % 128) return 0;
+  return mx_scale_bytes(rows, K);
+}
+
+int vcap_mx_quantize(int in_dtype, const void* x, int64_t ldx, int rows, int K, void* q, uint8_t* scales,
+                     void* stream) {
+  if (!x || !q || !scales || rows <= 0 || K <= 0 || ldx < K) return fail(VCAP_E_ARG, "vcap_mx_quantize: bad arguments");
+  if (in_dtype != VCAP_DT_F32 && in_dtype != VCAP_DT_BF16) return fail(VCAP_E_ARG, "vcap_mx_quantize: in_dtype");
+  if (K % 256) return fail(VCAP_E_UNSUPPORTED, "vcap_mx_quantize: K must be a multiple of 256");
+  VCAP_TRY(vcap_mx_quantize_dispatch(in_dtype, x, (long)ldx, rows, K, (uint8_t*)q, scales, rows, (hipStream_t)stream),
+           "vcap_mx_quantize");
+  return 0;
+}
+
+int vcap_layernorm_mx(const float* x, int64_t ldx, void* q, uint8_t* scales, const float* gamma, const float* beta,
+                      int rows, int dim, float eps, void* stream) {
+  if (!x || !q || !scales || rows <= 0 || dim <= 0 || ldx < dim) return fail(VCAP_E_ARG, "vcap_layernorm_mx: bad arguments");
+  if ((gamma == nullptr) != (beta == nullptr)) return fail(VCAP_E_ARG, "vcap_layernorm_mx: gamma/beta mismatch");
+  if (dim % 256 || dim > 1024) return fail(VCAP_E_UNSUPPORTED, "vcap_layernorm_mx: dim must be 256, 512, 768 or 1024");
+  VCAP_TRY(vcap_layernorm_mx_dispatch(x, (long)ldx, (uint8_t*)q, scales, rows, gamma, beta, rows, dim, eps,
+                                      (hipStream_t)stream),
+           "vcap_layernorm_mx");
+  return 0;
+}
+
+int vcap_gemm_mx(const void* A, const uint8_t* a_scales, const void* W, const uint8_t* w_scales, int out_dtype,
+                 void* C, int64_t ldc, uint8_t* c_scales, int M, int N, int K, const float* bias, int act,
+                 const float* res, void* stream) {
+  if (!A || !a_scales || !W || !w_scales || !C || M <= 0 || N <= 0 || K <= 0)
+    return fail(VCAP_E_ARG, "vcap_gemm_mx: bad arguments");
+  if (K % 256) return fail(VCAP_E_UNSUPPORTED, "vcap_gemm_mx: K must be a multiple of 256");
+  if (N % 16 || ldc < N || ldc % 16) return fail(VCAP_E_UNSUPPORTED, "vcap_gemm_mx: N and ldc must be multiples of 16");
+  if (out_dtype == VCAP_DT_MXFP8) {
+    if (act != 1 || !bias || !c_scales || res || N % 128)
+      return fail(VCAP_E_UNSUPPORTED, "vcap_gemm_mx: MXFP8 output needs bias + gelu (act=1), c_scales, N % 128 == 0");
+  } else if (out_dtype != VCAP_DT_BF16 && out_dtype != VCAP_DT_F32) {
+    return fail(VCAP_E_ARG, "vcap_gemm_mx: out_dtype");
+  }
+  if (res && out_dtype != VCAP_DT_F32) return fail(VCAP_E_UNSUPPORTED, "vcap_gemm_mx: residual needs f32 output");
+  if (act < 0 || act > 1) return fail(VCAP_E_ARG, "vcap_gemm_mx: act must be 0 or 1");
+  GemmEpi e{bias, res, (long)ldc, act, res ? 1 : 0, 0, 0, 0, 0, a_scales, w_scales, c_scales};
+  g_err.clear();
+  VCAP_TRY(vcap_gemm_dispatch(VCAP_DT_MXFP8, out_dtype, A, K, W, K, C, ldc, M, N, K, e, (hipStream_t)stream),
+           "vcap_gemm_mx");
+  return 0;
+}
+
 static int ensure_attn_lds() {
   if (attn_lds_configured) return 0;
   attn_lds_configured = true;
@@ -434,37 +500,47 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
   Carver c(workspace);
   VitBufs w = carve_vit(c, d, B, T);
   const int dt = d->dtype, D = d->dim, g = d->image / d->patch, P = g * g, N = P + 1, BT = B * T;
+  const int adt = vit_adt(dt);
+  const bool mx = dt == VCAP_DT_MXFP8;
   const int M = BT * N;
   // patch embedding: im2col + GEMM whose epilogue adds bias + pos[1+p] and scatters row bt*N+1+p
-  VCAP_TRY(vcap_patchify_dispatch(dt, frames, w.act, w.x, d->cls, d->pos, BT, d->image, d->patch, d->kpad, N, D, s),
+  VCAP_TRY(vcap_patchify_dispatch(adt, frames, w.act, w.x, d->cls, d->pos, BT, d->image, d->patch, d->kpad, N, D, s),
            "patchify");
   GemmEpi pe{d->patch_b, d->pos, D, 0, 2, P, N, 1, 1};
-  VCAP_TRY(vcap_gemm_dispatch(dt, VCAP_DT_F32, w.act, d->kpad, d->patch_w, d->kpad, w.x, D, BT * P, D, d->kpad, pe, s),
+  VCAP_TRY(vcap_gemm_dispatch(adt, VCAP_DT_F32, w.act, d->kpad, d->patch_w, d->kpad, w.x, D, BT * P, D, d->kpad, pe, s),
            "patch_gemm");
   for (int l = 0; l < d->depth; ++l) {
     const vcap_vit_layer& ly = d->layers[l];
-    VCAP_TRY(vcap_layernorm_dispatch(dt, w.x, D, w.xn, D, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s), "norm1");
-    GemmEpi e1{ly.qkv_b, nullptr, 0, 0, 0, 0, 0, 0, 0};
+    if (mx)
+      VCAP_TRY(vcap_layernorm_mx_dispatch(w.x, D, (uint8_t*)w.xn, w.xn_s, M, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s),
+               "norm1");
+    else
+      VCAP_TRY(vcap_layernorm_dispatch(dt, w.x, D, w.xn, D, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s), "norm1");
+    GemmEpi e1{ly.qkv_b, nullptr, 0, 0, 0, 0, 0, 0, 0, w.xn_s, ly.qkv_ws, nullptr};
     {
       ProbeScope ps("vit.qkv", s);
-      VCAP_TRY(vcap_gemm_dispatch(dt, dt, w.xn, D, ly.qkv_w, D, w.qkv, 3 * D, M, 3 * D, D, e1, s), "qkv");
+      VCAP_TRY(vcap_gemm_dispatch(dt, adt, w.xn, D, ly.qkv_w, D, w.qkv, 3 * D, M, 3 * D, D, e1, s), "qkv");
     }
     {
       ProbeScope ps("vit.attention", s);
-      VCAP_TRY(vcap_vit_attention_dispatch(dt, w.qkv, w.attn, BT, N, d->heads, s), "attention");
+      VCAP_TRY(vcap_vit_attention_dispatch(adt, w.qkv, w.attn, BT, N, d->heads, s), "attention");
     }
     GemmEpi e2{ly.proj_b, w.x, D, 0, 1, 0, 0, 0, 0};
     {
       ProbeScope ps("vit.proj", s);
-      VCAP_TRY(vcap_gemm_dispatch(dt, VCAP_DT_F32, w.attn, D, ly.proj_w, D, w.x, D, M, D, D, e2, s), "attn_proj");
+      VCAP_TRY(vcap_gemm_dispatch(adt, VCAP_DT_F32, w.attn, D, ly.proj_w, D, w.x, D, M, D, D, e2, s), "attn_proj");
     }
-    VCAP_TRY(vcap_layernorm_dispatch(dt, w.x, D, w.xn, D, ly.ln2_g, ly.ln2_b, M, D, d->ln_eps, s), "norm2");
-    GemmEpi e3{ly.fc1_b, nullptr, 0, 1, 0, 0, 0, 0, 0};
+    if (mx)
+      VCAP_TRY(vcap_layernorm_mx_dispatch(w.x, D, (uint8_t*)w.xn, w.xn_s, M, ly.ln2_g, ly.ln2_b, M, D, d->ln_eps, s),
+               "norm2");
+    else
+      VCAP_TRY(vcap_layernorm_dispatch(dt, w.x, D, w.xn, D, ly.ln2_g, ly.ln2_b, M, D, d->ln_eps, s), "norm2");
+    GemmEpi e3{ly.fc1_b, nullptr, 0, 1, 0, 0, 0, 0, 0, w.xn_s, ly.fc1_ws, w.act_s};
     {
       ProbeScope ps("vit.fc1", s);
       VCAP_TRY(vcap_gemm_dispatch(dt, dt, w.xn, D, ly.fc1_w, D, w.act, d->mlp, M, d->mlp, D, e3, s), "fc1");
     }
-    GemmEpi e4{ly.fc2_b, w.x, D, 0, 1, 0, 0, 0, 0};
+    GemmEpi e4{ly.fc2_b, w.x, D, 0, 1, 0, 0, 0, 0, w.act_s, ly.fc2_ws, nullptr};
     {
       ProbeScope ps("vit.fc2", s);
       VCAP_TRY(vcap_gemm_dispatch(dt, VCAP_DT_F32, w.act, d->mlp, ly.fc2_w, d->mlp, w.x, D, M, D, d->mlp, e4, s), "fc2");

@@ -143,9 +143,93 @@ VCAP_DEV f32x4 mfma_frag(const u32x4& a, const u32x4& b, f32x4 c, float*) {
   return c;
 }
 
+// ---- MXFP8: OCP e4m3fn elements with one E8M0 (power-of-two) scale per 32 consecutive K
+// elements of a row, the gfx950-native block-scaled format the v_mfma_scale_f32_16x16x128_f8f6f4
+// instruction consumes at twice the bf16 MFMA rate.  Element value = fp8 * 2^(scale - 127).
+// Scales are stored in the order the 256x256 GEMM consumes them: per (128-wide K-tile, group of
+// 256 rows) one contiguous 1 KiB block laid out [k-block 0..3][row % 16][row / 16 (0..15)], so a
+// workgroup stages a K-tile's scales for its 256 rows with one 4-byte LDS-DMA per thread and a
+// lane reads the scales of its 4 row sub-tiles (one per MFMA, picked by OPSEL) in one ds_read.
+VCAP_DEV long mx_scale_index(int row, int k, int groups) {
+  return ((long)((k >> 7) * groups + (row >> 8)) * 4 + ((k >> 5) & 3)) * 256 + (row & 15) * 16 + ((row >> 4) & 15);
+}
+typedef uint8_t fp8_t;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(8))) unsigned int u32x8;
+
+VCAP_DEV u32x8 cat8(const u32x4& lo, const u32x4& hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+VCAP_DEV u32x4 lo4(const u32x8& v) { return __builtin_shufflevector(v, v, 0, 1, 2, 3); }
+VCAP_DEV u32x4 hi4(const u32x8& v) { return __builtin_shufflevector(v, v, 4, 5, 6, 7); }
+
+// E8M0 scale of a 32-block from its max |x|: 2^(floor(log2 amax) - 7), so every scaled element
+// lies in (-256, 256) - inside e4m3's 448 range, no saturation - and the block max keeps e4m3's
+// full 3-bit mantissa.  amax == 0 (or subnormal) gives the smallest scale.
+VCAP_DEV int mx_scale_byte(float amax) {
+  const int e = (int)((__float_as_uint(amax) >> 23) & 0xFF) - 7;
+  return e < 0 ? 0 : e;  // finite amax: e <= 247
+}
+// 2^-(scale - 127) as an f32 multiplier (exact power of two; exponent field 254 - byte >= 7)
+VCAP_DEV float mx_inv_scale(int byte) { return __uint_as_float((uint32_t)(254 - byte) << 23); }
+
+// four f32 (already multiplied by the inverse scale) -> four e4m3 bytes, round-to-nearest-even
+VCAP_DEV uint32_t pack_fp8x4(float a, float b, float c, float d) {
+  int r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  return (uint32_t)r;
+}
+
+// D += (A * 2^(sa-127)) . (B * 2^(sb-127)) over K = 128.  Operand layout (measured on gfx950,
+// tools/mx_layout_probe.hip): lane l holds row / column (l & 15), K elements [16 g, +16) in its
+// bytes 0-15 and [64 + 16 g, +16) in bytes 16-31 (g = l >> 4); the scale in byte SA / SB of
+// lane l's sa / sb applies to K block [32 g, +32) of row / column (l & 15).
+//
+// Issued as inline asm with the accumulator tied ("+v"): the builtin's register allocation does
+// not keep D == C for this instruction, and in the 256x256 GEMM (128 accumulator registers)
+// that turns into hundreds of spills.  The compiler's hazard recognizer cannot see inside the
+// asm, so callers put >= 2 wait states between VALU writes of the operands and the MFMA and
+// >= 18 between the last MFMA and VALU reads of its result (mfma_mx_drain()).
+template <int SA, int SB>
+VCAP_DEV void mfma_mx(const u32x8& a, int sa, const u32x8& b, int sb, f32x4& c);
+#define VCAP_MX_SPEC(SA, SB, A0, A1, B0, B1)                                                         \
+  template <>                                                                                       \
+  VCAP_DEV void mfma_mx<SA, SB>(const u32x8& a, int sa, const u32x8& b, int sb, f32x4& c) {         \
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[" #A0 "," #B0     \
+                 ",0] op_sel_hi:[" #A1 "," #B1 ",0]"                                                \
+                 : "+v"(c)                                                                          \
+                 : "v"(a), "v"(b), "v"(sa), "v"(sb));                                               \
+  }
+#define VCAP_MX_ROW(SA, A0, A1)             \
+  VCAP_MX_SPEC(SA, 0, A0, A1, 0, 0)         \
+  VCAP_MX_SPEC(SA, 1, A0, A1, 1, 0)         \
+  VCAP_MX_SPEC(SA, 2, A0, A1, 0, 1)         \
+  VCAP_MX_SPEC(SA, 3, A0, A1, 1, 1)
+VCAP_MX_ROW(0, 0, 0)
+VCAP_MX_ROW(1, 1, 0)
+VCAP_MX_ROW(2, 0, 1)
+VCAP_MX_ROW(3, 1, 1)
+#undef VCAP_MX_ROW
+#undef VCAP_MX_SPEC
+// Quantise 4 consecutive f32 (columns c..c+3 of `row`) held by lanes in groups of 8 (one 32-block
+// per 8 lanes, lane-contiguous): block max |x| by DPP within the 8 lanes, E8M0 scale, 4 e4m3 bytes.
+// Every lane of the wave must be active.
+VCAP_DEV void mx_quant_store4(f32x4 o, int row, int c, fp8_t* yrow, uint8_t* scales, int groups) {
+  float amax = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+  amax = fmaxf(amax, dpp_f<DPP_XOR1>(amax));
+  amax = fmaxf(amax, dpp_f<DPP_XOR2>(amax));
+  amax = fmaxf(amax, dpp_f<DPP_HALF_MIRROR>(amax));
+  const int sb = mx_scale_byte(amax);
+  const float inv = mx_inv_scale(sb);
+  *reinterpret_cast<uint32_t*>(yrow + c) = pack_fp8x4(o.x * inv, o.y * inv, o.z * inv, o.w * inv);
+  if ((threadIdx.x & 7) == 0) scales[mx_scale_index(row, c, groups)] = (uint8_t)sb;
+}
+
+VCAP_DEV void mfma_mx_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
+
 // elements of T per 16-byte fragment chunk
 template <typename T> struct Frag { static constexpr int kElems = 16 / sizeof(T); };
 
 #ifndef VCAP_H_
-enum { VCAP_DT_F32 = 0, VCAP_DT_BF16 = 1 };  // mirrors include/vcap.h
+enum { VCAP_DT_F32 = 0, VCAP_DT_BF16 = 1, VCAP_DT_MXFP8 = 2 };  // mirrors include/vcap.h
 #endif

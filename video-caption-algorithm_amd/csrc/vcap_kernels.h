@@ -10,6 +10,11 @@ struct GemmEpi {
   int res_mode;       // 0 none, 1 residual row == output row (may alias C), 2 row (m % G) + roff
   int G, Gs, goff;    // output row remap: G ? (m/G)*Gs + goff + m%G : m
   int roff;
+  // MXFP8 operands (in_dt == VCAP_DT_MXFP8): E8M0 block scales of A and W, K-tile-major
+  // (vcap_common.h); c_scale receives the scales of an MXFP8 output (act must be gelu).
+  const uint8_t* a_scale;
+  const uint8_t* w_scale;
+  uint8_t* c_scale;
 };
 
 enum { PRO_LN = 0, PRO_DIRECT = 1 };
@@ -53,6 +58,11 @@ bool vcap_gemm256_ok(int in_dt, int out_dt, long lda, long ldw, long ldc, int M,
 hipError_t vcap_gemm256_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
                                  long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s);
 void vcap_gemm_set_policy(int p);
+hipError_t vcap_layernorm_mx_dispatch(const float* x, long ldx, uint8_t* q, uint8_t* scales, int srows,
+                                      const float* gamma, const float* beta, int rows, int D, float eps,
+                                      hipStream_t s);
+hipError_t vcap_mx_quantize_dispatch(int in_dt, const void* x, long ldx, int rows, int K, uint8_t* q,
+                                     uint8_t* scales, int srows, hipStream_t s);
 hipError_t vcap_layernorm_dispatch(int out_dt, const float* x, long ldx, void* y, long ldy, const float* gamma,
                                    const float* beta, int rows, int D, float eps, hipStream_t s);
 hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s);

@@ -15,8 +15,8 @@ from pathlib import Path
 _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
-DT_F32, DT_BF16 = 0, 1
-ABI_VERSION = 2
+DT_F32, DT_BF16, DT_MXFP8 = 0, 1, 2
+ABI_VERSION = 3
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
@@ -28,7 +28,8 @@ class VcapError(RuntimeError):
 
 class VitLayer(C.Structure):
     _fields_ = [("ln1_g", vp), ("ln1_b", vp), ("qkv_w", vp), ("qkv_b", vp), ("proj_w", vp), ("proj_b", vp),
-                ("ln2_g", vp), ("ln2_b", vp), ("fc1_w", vp), ("fc1_b", vp), ("fc2_w", vp), ("fc2_b", vp)]
+                ("ln2_g", vp), ("ln2_b", vp), ("fc1_w", vp), ("fc1_b", vp), ("fc2_w", vp), ("fc2_b", vp),
+                ("qkv_ws", vp), ("fc1_ws", vp), ("fc2_ws", vp)]
 
 
 class VitDesc(C.Structure):
@@ -73,6 +74,10 @@ SIGNATURES = {
                         i32, vp]),
     "vcap_layernorm": (i32, [i32, vp, i64, vp, i64, vp, vp, i32, i32, f32, vp]),
     "vcap_vit_attention": (i32, [i32, vp, vp, i32, i32, i32, vp]),
+    "vcap_mx_scale_bytes": (sz, [i32, i32]),
+    "vcap_mx_quantize": (i32, [i32, vp, i64, i32, i32, vp, vp, vp]),
+    "vcap_layernorm_mx": (i32, [vp, i64, vp, vp, vp, vp, i32, i32, f32, vp]),
+    "vcap_gemm_mx": (i32, [vp, vp, vp, vp, i32, vp, i64, vp, i32, i32, i32, vp, i32, vp, vp]),
     "vcap_vit_pool_temporal": (i32, [i32, vp, vp, i32, i32, i32, i32, i32, vp]),
     "vcap_prefix_project": (i32, [vp, i32, i32, C.POINTER(PrefixDesc), vp, vp]),
     "vcap_rows_packed_bytes": (sz, [i32, i32, i32]),

@@ -24,6 +24,9 @@ from . import _native as N
 from .configs import VIDEO_DIM, GPT2Arch, ViTArch
 
 _DTYPES = {"bf16": (N.DT_BF16, torch.bfloat16), "fp32": (N.DT_F32, torch.float32)}
+# ViT only: "fp8" = MXFP8 block GEMMs (QKV / fc1 / fc2: e4m3 + E8M0 per 32 K elements, the gfx950
+# scaled-MFMA format; BASELINE configs[4]); patch-embed, attention and attn-proj run in bf16.
+_VIT_DTYPES = dict(_DTYPES, fp8=(N.DT_MXFP8, torch.bfloat16))
 
 
 def _dtype(mode: str):
@@ -54,7 +57,10 @@ class HipViTEncoder:
                  video_dim: int = VIDEO_DIM):
         N.lib()
         self.arch, self.precision, self.device = arch, precision, torch.device(device)
-        self.dt, tdt = _dtype(precision)
+        if precision not in _VIT_DTYPES:
+            raise ValueError(f"precision must be one of {sorted(_VIT_DTYPES)}, got {precision!r}")
+        self.dt, tdt = _VIT_DTYPES[precision]
+        mx = self.dt == N.DT_MXFP8
         self.video_dim = video_dim
         p = "encoder.backbone."
         dev = self.device
@@ -68,7 +74,17 @@ class HipViTEncoder:
         def wt(k, shape=None):
             return f32(k, shape).to(tdt).contiguous()
 
-        kstep = 64 if self.dt == N.DT_BF16 else 32
+        def wmx(k):
+            """-> (e4m3 [N, K] uint8, E8M0 scales) through vcap_mx_quantize (kept alive in _keep)."""
+            w = f32(k)
+            n, kk = w.shape
+            q = torch.empty(n, kk, dtype=torch.uint8, device=dev)
+            sc = torch.empty(int(N.lib().vcap_mx_scale_bytes(n, kk)), dtype=torch.uint8, device=dev)
+            N.check(N.lib().vcap_mx_quantize(N.DT_F32, w.data_ptr(), kk, n, kk, q.data_ptr(), sc.data_ptr(),
+                                             _stream(dev)), "vcap_mx_quantize")
+            return q, sc
+
+        kstep = 32 if self.dt == N.DT_F32 else 64
         K = arch.patch_k
         self.kpad = ((K + 63) // 64) * 64 if kstep == 64 else ((K + 31) // 32) * 32
         pw = torch.zeros(arch.dim, self.kpad, dtype=torch.float32)
@@ -90,11 +106,15 @@ class HipViTEncoder:
         for i in range(arch.depth):
             b = f"{p}blocks.{i}."
             lt = dict(ln1_g=f32(b + "norm1.weight"), ln1_b=f32(b + "norm1.bias"),
-                      qkv_w=wt(b + "attn.qkv.weight"), qkv_b=f32(b + "attn.qkv.bias"),
+                      qkv_b=f32(b + "attn.qkv.bias"),
                       proj_w=wt(b + "attn.proj.weight"), proj_b=f32(b + "attn.proj.bias"),
                       ln2_g=f32(b + "norm2.weight"), ln2_b=f32(b + "norm2.bias"),
-                      fc1_w=wt(b + "mlp.fc1.weight"), fc1_b=f32(b + "mlp.fc1.bias"),
-                      fc2_w=wt(b + "mlp.fc2.weight"), fc2_b=f32(b + "mlp.fc2.bias"))
+                      fc1_b=f32(b + "mlp.fc1.bias"), fc2_b=f32(b + "mlp.fc2.bias"))
+            for name, key in (("qkv", "attn.qkv.weight"), ("fc1", "mlp.fc1.weight"), ("fc2", "mlp.fc2.weight")):
+                if mx:
+                    lt[name + "_w"], lt[name + "_ws"] = wmx(b + key)
+                else:
+                    lt[name + "_w"] = wt(b + key)
             for k, v in lt.items():
                 keep(v)
                 setattr(self.layers[i], k, v.data_ptr())

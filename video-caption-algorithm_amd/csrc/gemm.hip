@@ -173,6 +173,18 @@ static hipError_t launch_gemm(const void* A, long lda, const void* W, long ldw, 
 static int g_gemm_policy = 0;  // 0 auto, 1 always the 128x128 kernel, 2 the 256x256 kernel where it applies
 void vcap_gemm_set_policy(int p) { g_gemm_policy = p; }
 
+// CUs the stream's kernels may use (hipExtStreamGetCUMask; the encode stream of the overlapped
+// pipeline is CU-masked), so the round arithmetic below matches what the stream really gets.
+int vcap_stream_cus(hipStream_t s) {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  uint32_t mask[16] = {0};
+  if (hipExtStreamGetCUMask(s, 16, mask) != hipSuccess) return ncu;
+  int n = 0;
+  for (int i = 0; i < 16; ++i) n += __builtin_popcount(mask[i]);
+  return n > 0 && n < ncu ? n : ncu;
+}
+
 // in_dt: operand dtype; out_dt: C dtype (the residual stream is f32)
 hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
                               long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s) {
@@ -187,7 +199,7 @@ hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, co
     const int tn = (N + 255) / 256;
     const long tiles256 = (long)((M + 255) / 256) * tn;
     if (g_gemm_policy == 2) return vcap_gemm256_dispatch(in_dt, out_dt, A, lda, W, ldw, C, ldc, M, N, K, epi, s);
-    const int ncu = 256;
+    const int ncu = vcap_stream_cus(s);
     if (tiles256 >= ncu) {
       const long rounds = tiles256 / ncu;
       const long rem = tiles256 - rounds * ncu;

@@ -338,8 +338,8 @@ int vcap_stream_create_cu_reserved(int reserve_cus, void** stream) {
   int ncu = 0;
   VCAP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "cu count");
   if (reserve_cus >= ncu) return fail(VCAP_E_ARG, "cannot reserve every CU");
-  // The driver spreads consecutive mask bits across XCDs / shader engines, so clearing the first
-  // `reserve_cus` bits leaves an even slice of every XCD to the other streams.
+  // Consecutive mask bits fill one XCD (32 CUs) before the next (measured: tools/decode_xcd_sweep.py),
+  // so clearing the first `reserve_cus` bits hands whole XCDs - and their L2s - to the other streams.
   std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
   for (int c = reserve_cus; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
   hipStream_t s = nullptr;

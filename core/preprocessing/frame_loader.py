@@ -1,8 +1,9 @@
 """frames_dir -> [1, T, 3, H, W] tensor (behaviour of reference core/preprocessing/frame_loader.py:13-49).
 
-Strided pick files[::max(n // T, 1)][:T] of sorted frame_*.jpg, PIL bilinear resize to (H, W)
-(what torchvision Resize does for PIL images), /255, ImageNet mean/std normalisation.  torchvision
-is not required.  Frames are uploaded once; the HIP encoder consumes them from HBM.
+Strided pick files[::max(n // T, 1)][:T] of sorted frame_*.jpg, decoded by PIL on the host; the
+Resize((S, S)) -> ToTensor -> Normalize chain runs on the GPU (vcap.preprocess, bit-identical to
+PIL's BILINEAR resample + the f32 normalisation) for a cuda `device`.  `backend="pil"` keeps the
+per-frame host chain (PIL resize + numpy), e.g. for a CPU-only caller.  torchvision is not required.
 """
 from __future__ import annotations
 
@@ -28,16 +29,28 @@ def _to_chw(img, size: int) -> np.ndarray:
     return ((arr - _MEAN) / _STD).transpose(2, 0, 1)
 
 
-def load_video_tensor(frames_dir, num_frames: int, image_size: int, device: str = "cuda") -> torch.Tensor:
+def load_video_tensor(frames_dir, num_frames: int, image_size: int, device: str = "cuda",
+                      backend: str = "auto") -> torch.Tensor:
     from PIL import Image
     files = list_frames(frames_dir)
     if not files:
         raise FileNotFoundError(f"No frame_*.jpg files found under {frames_dir}")
     picks = files[::max(len(files) // num_frames, 1)][:num_frames]
-    frames = []
+    on_gpu = torch.device(device).type == "cuda"
+    if backend == "auto":
+        backend = "hip" if on_gpu else "pil"
+    if backend not in ("hip", "pil"):
+        raise ValueError(f"backend must be 'auto', 'hip' or 'pil', got {backend!r}")
+    decoded = []
     for p in picks:
         with Image.open(p) as im:
-            frames.append(_to_chw(im, image_size))
-    video = torch.from_numpy(np.stack(frames)[None]).to(device)
+            decoded.append(np.asarray(im.convert("RGB")) if backend == "hip" else _to_chw(im, image_size))
+    if backend == "hip":
+        from vcap.preprocess import frames_to_video
+        if len({d.shape for d in decoded}) != 1:
+            raise ValueError("frames of one video must share one size")
+        video = frames_to_video(decoded, image_size, device)
+    else:
+        video = torch.from_numpy(np.stack(decoded)[None]).to(device)
     log.info("frames_dir=%s total=%s sampled=%s", frames_dir, len(files), len(picks))
     return video

@@ -20,6 +20,7 @@
  *                           src/models/video_encoder.py:112-174 (fused SDPA, tanh-GELU MLP,
  *                           in-place residual) - op-level entry points for the plugin registry
  *                           (core/operators/trt_plugin_hooks.py:7-34)
+ *   vcap_frames_preprocess  core/preprocessing/frame_loader.py:34-45 (Resize -> ToTensor -> Normalize)
  *   vcap_vit_encode         ViTFrameEncoder.forward (src/models/video_encoder.py:288-326) fused with
  *                           the engine prefix (core/engine.py:43-50) and the mapper
  *   vcap_gpt2_generate      GPT2TextDecoder.generate (src/models/text_decoder.py:105-146) ->
@@ -145,6 +146,16 @@ int vcap_gemm(int in_dtype, int out_dtype, const void* A, int64_t lda, const voi
 int vcap_layernorm(int out_dtype, const float* x, int64_t ldx, void* y, int64_t ldy, const float* gamma,
                    const float* beta, int rows, int dim, float eps, void* stream);
 int vcap_vit_attention(int dtype, const void* qkv, void* out, int frames, int tokens, int heads, void* stream);
+
+/* ---- frame preprocessing (core/preprocessing/frame_loader.py:34-45: torchvision Resize((S, S)) on
+ *      PIL images -> ToTensor -> Normalize): decoded RGB frames uint8 [n, in_h, in_w, 3] (device)
+ *      -> out f32 [n, 3, out_h, out_w] (normalised) and/or out_u8 [n, out_h, out_w, 3] (the resized
+ *      pixels), bit-identical to PIL Image.resize(BILINEAR) + the f32 /255, -mean, /std chain.
+ *      mean3 / std3 are HOST arrays of 3 floats.  Downscale factors up to 31. ---- */
+size_t vcap_frames_workspace_bytes(int n, int in_h, int in_w, int out_h, int out_w);
+int vcap_frames_preprocess(const uint8_t* frames, int n, int in_h, int in_w, int out_h, int out_w, const float* mean3,
+                           const float* std3, float* out, uint8_t* out_u8, void* workspace, size_t ws_bytes,
+                           void* stream);
 
 /* ---- MXFP8 (BASELINE configs[4]: fp8 MFMA path for the ViT GEMMs) ----
  * vcap_mx_quantize: rows of f32 / bf16 [rows, K] (row stride ldx) -> e4m3 [rows, K] + scales.

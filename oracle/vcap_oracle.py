@@ -327,3 +327,83 @@ def mx_pack_scales(sb: np.ndarray) -> np.ndarray:
 
 def mx_unpack_scales(flat: np.ndarray, rows: int, K: int) -> np.ndarray:
     return np.asarray(flat)[mx_scale_index(rows, K)]
+
+
+# ----------------------------------------------------------------------------- frame preprocessing
+# Reference: core/preprocessing/frame_loader.py:34-45 - torchvision Resize((S, S)) on a PIL image
+# (= PIL Image.resize(BILINEAR), Pillow 12.2 in this image) -> ToTensor (/255 in f32) ->
+# Normalize(mean, std) (f32 sub, div).  Restated here from Pillow's Resample.c algorithm
+# (precompute_coeffs / normalize_coeffs_8bpc / ImagingResample{Horizontal,Vertical}_8bpc): separable
+# triangle filter widened by the downscale factor, double-precision weights normalised per output
+# pixel, converted to 22-bit fixed point, int32 accumulation from a 2^21 rounding bias, clamp to
+# [0, 255] after each pass (horizontal pass first, over the source rows the vertical pass uses).
+
+_PREC = 22
+
+
+def _pil_coeffs(in_size: int, out_size: int):
+    scale = in_size / out_size
+    fscale = max(scale, 1.0)
+    support = 1.0 * fscale
+    ksize = int(math.ceil(support)) * 2 + 1
+    bounds = np.zeros((out_size, 2), np.int64)
+    kk = np.zeros((out_size, ksize), np.int64)
+    for xx in range(out_size):
+        center = (xx + 0.5) * scale
+        ss = 1.0 / fscale
+        xmin = max(int(center - support + 0.5), 0)
+        xmax = min(int(center + support + 0.5), in_size) - xmin
+        w = []
+        for x in range(xmax):
+            t = abs((x + xmin - center + 0.5) * ss)
+            w.append(1.0 - t if t < 1.0 else 0.0)
+        ww = sum(w) if w else 0.0  # left-to-right double sum, as the C loop
+        acc = 0.0
+        for v in w:
+            acc += v
+        ww = acc
+        for x in range(xmax):
+            v = w[x] / ww if ww != 0.0 else w[x]
+            kk[xx, x] = int(-0.5 + v * (1 << _PREC)) if v < 0 else int(0.5 + v * (1 << _PREC))
+        bounds[xx] = (xmin, xmax)
+    return bounds, kk
+
+
+def _pil_pass(img: np.ndarray, bounds, kk, axis: int) -> np.ndarray:
+    """One 8-bpc resample pass along `axis` (0 rows, 1 columns) of an [H, W, C] uint8 image."""
+    src = np.moveaxis(img.astype(np.int64), axis, 0)
+    out = np.empty((len(bounds),) + src.shape[1:], np.uint8)
+    for i, (lo, n) in enumerate(bounds):
+        acc = np.full(src.shape[1:], 1 << (_PREC - 1), np.int64)
+        for t in range(n):
+            acc += src[lo + t] * kk[i, t]
+        out[i] = np.clip(acc >> _PREC, 0, 255)
+    return np.moveaxis(out, 0, axis)
+
+
+def pil_resize_bilinear(img: np.ndarray, out_w: int, out_h: int) -> np.ndarray:
+    """[H, W, 3] uint8 -> [out_h, out_w, 3] uint8, bit-identical to PIL Image.resize(BILINEAR)."""
+    h, w = img.shape[:2]
+    if (h, w) == (out_h, out_w):
+        return img.copy()
+    bh, kh = _pil_coeffs(w, out_w)
+    bv, kv = _pil_coeffs(h, out_h)
+    if w != out_w:
+        y0, y1 = int(bv[0, 0]), int(bv[-1, 0] + bv[-1, 1])
+        img = _pil_pass(img[y0:y1], bh, kh, axis=1)
+        bv = bv.copy()
+        bv[:, 0] -= y0
+    if h != out_h:
+        img = _pil_pass(img, bv, kv, axis=0)
+    return img
+
+
+def frames_to_tensor(imgs_u8: np.ndarray, size: int) -> np.ndarray:
+    """[T, H, W, 3] uint8 frames -> [T, 3, size, size] f32 (Resize -> ToTensor -> Normalize)."""
+    mean = np.array([0.485, 0.456, 0.406], np.float32)[:, None, None]
+    std = np.array([0.229, 0.224, 0.225], np.float32)[:, None, None]
+    out = []
+    for im in imgs_u8:
+        r = pil_resize_bilinear(im, size, size).transpose(2, 0, 1).astype(np.float32) / np.float32(255.0)
+        out.append((r - mean) / std)
+    return np.stack(out)

@@ -164,3 +164,15 @@ def test_oracle_mx_quantize_properties():
     nz = s > 0
     assert ((top[nz] >= 128) & (top[nz] < 256)).all()
     assert np.array_equal(O.mx_unpack_scales(O.mx_pack_scales(s), 300, 512), s)
+
+
+@pytest.mark.parametrize("hw", [(240, 320), (480, 640), (224, 224), (100, 150), (1080, 1920), (37, 500)])
+def test_oracle_pil_resize_matches_pillow(hw):
+    """The Resample.c restatement the GPU preprocessing kernel follows is bit-identical to PIL."""
+    from PIL import Image
+    h, w = hw
+    g = np.random.default_rng(h * 7 + w)
+    for img in (g.integers(0, 256, (h, w, 3), dtype=np.uint8),
+                (np.add.outer(np.arange(h), 3 * np.arange(w))[:, :, None] * np.array([1, 2, 5]) % 256).astype(np.uint8)):
+        ref = np.asarray(Image.fromarray(img).resize((224, 224), Image.BILINEAR))
+        assert np.array_equal(O.pil_resize_bilinear(img, 224, 224), ref)

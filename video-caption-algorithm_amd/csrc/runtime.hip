@@ -446,6 +446,26 @@ int vcap_gemm_mx(const void* A, const uint8_t* a_scales, const void* W, const ui
   return 0;
 }
 
+size_t vcap_frames_workspace_bytes(int n, int in_h, int in_w, int out_h, int out_w) {
+  if (n <= 0 || in_h <= 0 || in_w <= 0 || out_h <= 0 || out_w <= 0) return 0;
+  return vcap_frames_ws_bytes(n, in_h, in_w, out_h, out_w);
+}
+
+int vcap_frames_preprocess(const uint8_t* frames, int n, int in_h, int in_w, int out_h, int out_w, const float* mean3,
+                           const float* std3, float* out, uint8_t* out_u8, void* workspace, size_t ws_bytes,
+                           void* stream) {
+  if (!frames || n <= 0 || in_h <= 0 || in_w <= 0 || out_h <= 0 || out_w <= 0 || !mean3 || !std3 || (!out && !out_u8))
+    return fail(VCAP_E_ARG, "vcap_frames_preprocess: bad arguments");
+  if (in_w > 31 * out_w || in_h > 31 * out_h)
+    return fail(VCAP_E_UNSUPPORTED, "vcap_frames_preprocess: downscale factor above 31");
+  if (ws_bytes < vcap_frames_ws_bytes(n, in_h, in_w, out_h, out_w))
+    return fail(VCAP_E_WORKSPACE, "vcap_frames_preprocess: workspace too small");
+  VCAP_TRY(vcap_frames_preprocess_dispatch(frames, n, in_h, in_w, out_h, out_w, mean3, std3, out, out_u8, workspace,
+                                           (hipStream_t)stream),
+           "vcap_frames_preprocess");
+  return 0;
+}
+
 static int ensure_attn_lds() {
   if (attn_lds_configured) return 0;
   attn_lds_configured = true;

@@ -91,3 +91,7 @@ hipError_t vcap_embed_tokens_dispatch(int dt, const int* tok, int rows, const vo
                                       int E, int pos, hipStream_t s);
 hipError_t vcap_kv_gather_dispatch(int dt, const void* src_pool, void* dst_pool, const int* src_rows, int rows, int maxp,
                                    int H, int len, long layer_elems, int L, hipStream_t s);
+size_t vcap_frames_ws_bytes(int n, int in_h, int in_w, int out_h, int out_w);
+hipError_t vcap_frames_preprocess_dispatch(const uint8_t* frames, int n, int in_h, int in_w, int out_h, int out_w,
+                                           const float* mean3, const float* std3, float* out, uint8_t* out_u8,
+                                           void* ws, hipStream_t s);

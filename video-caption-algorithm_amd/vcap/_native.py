@@ -74,6 +74,8 @@ SIGNATURES = {
                         i32, vp]),
     "vcap_layernorm": (i32, [i32, vp, i64, vp, i64, vp, vp, i32, i32, f32, vp]),
     "vcap_vit_attention": (i32, [i32, vp, vp, i32, i32, i32, vp]),
+    "vcap_frames_workspace_bytes": (sz, [i32, i32, i32, i32, i32]),
+    "vcap_frames_preprocess": (i32, [vp, i32, i32, i32, i32, i32, fp, fp, vp, vp, vp, sz, vp]),
     "vcap_mx_scale_bytes": (sz, [i32, i32]),
     "vcap_mx_quantize": (i32, [i32, vp, i64, i32, i32, vp, vp, vp]),
     "vcap_layernorm_mx": (i32, [vp, i64, vp, vp, vp, vp, i32, i32, f32, vp]),

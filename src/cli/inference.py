@@ -48,7 +48,8 @@ def parse(argv=None):
     ap.add_argument("--num_frames", type=int, default=16)
     ap.add_argument("--vit_name", default="vit_base_patch16_224")
     ap.add_argument("--gpt2_name", default="gpt2")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp8"],
+                    help="fp8 = MXFP8 ViT GEMMs (decoder bf16); fp32 = the parity mode")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--preset", default="", help="decode a single candidate with this preset (precise/detailed/"
                                                  "natural/safe_sample); default runs the 3-candidate infer()")

@@ -114,7 +114,9 @@ class HipVideoCaptionModel:
         self.hip_encoder = HipViTEncoder(sd, self.vit_arch, precision, self.device)
         self.encoder = _Encoder(self.hip_encoder)
         self.proj = _Identity()
-        self.decoder = HipTextDecoder(sd, self.gpt2_arch, precision, self.device, prefix_len, tokenizer_dir,
+        # "fp8" is a ViT-only mode (MXFP8 block GEMMs); the decoder then runs in bf16
+        self.decoder = HipTextDecoder(sd, self.gpt2_arch, "bf16" if precision == "fp8" else precision, self.device,
+                                      prefix_len, tokenizer_dir,
                                       use_graph)
         self._engine_prefix = HipPrefix(sd, self.gpt2_arch.n_embd, prefix_len, 0.6, 0.4, self.device)
 

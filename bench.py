@@ -191,7 +191,7 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "captions/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": {"bf16": "bf16", "fp8": "mxfp8-e4m3 (ViT QKV/fc1/fc2) + bf16"}.get(args.precision, "f32"),
+            "scaling": "weak", "vs_baseline": None, "dtype": {"bf16": "bf16", "fp8": "mxfp8-e4m3 (ViT QKV/proj/fc1/fc2) + bf16"}.get(args.precision, "f32"),
             "data": "synthetic (seeded U[0,1) frames, ImageNet-normalised; seeded random-init weights)",
             "config": {"workload": f"batch={B} synthetic {T}x3x224x224 videos per GPU, {args.vit} + {args.gpt2}, "
                                    f"{args.decode} decode max_new {args.max_new} (BASELINE configs[1]"

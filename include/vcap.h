@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 3
+#define VCAP_ABI_VERSION 4
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -56,15 +56,15 @@ typedef struct vcap_vit_layer {
   const float* ln2_g; const float* ln2_b;
   const void* fc1_w; const float* fc1_b;     /* [4D, D] */
   const void* fc2_w; const float* fc2_b;     /* [D, 4D] */
-  /* dtype VCAP_DT_MXFP8 only: qkv_w / fc1_w / fc2_w are e4m3 and these their E8M0 scales
-   * (vcap_mx_quantize); proj_w and the patch-embed weight stay bf16 */
-  const uint8_t* qkv_ws; const uint8_t* fc1_ws; const uint8_t* fc2_ws;
+  /* dtype VCAP_DT_MXFP8 only: qkv_w / proj_w / fc1_w / fc2_w are e4m3 and these their E8M0
+   * scales (vcap_mx_quantize); the patch-embed weight stays bf16 */
+  const uint8_t* qkv_ws; const uint8_t* proj_ws; const uint8_t* fc1_ws; const uint8_t* fc2_ws;
 } vcap_vit_layer;
 
 typedef struct vcap_vit_desc {
-  int dtype;                 /* operand dtype of the block GEMMs (VCAP_DT_*; MXFP8: QKV / fc1 / fc2
-                                in MXFP8 with LayerNorm and GELU emitting MXFP8 operands, patch-embed,
-                                attention and attn-proj in bf16) */
+  int dtype;                 /* operand dtype of the block GEMMs (VCAP_DT_*; MXFP8: QKV / attn-proj /
+                                fc1 / fc2 in MXFP8 with LayerNorm, attention and GELU emitting MXFP8
+                                operands; patch-embed and the QK^T / PV products in bf16) */
   int dim, depth, heads, patch, image, mlp, video_dim;
   int kpad;                  /* patch K (3*p*p) padded to the GEMM K step */
   float ln_eps;              /* 1e-6 (timm) */
@@ -164,6 +164,10 @@ int vcap_frames_preprocess(const uint8_t* frames, int n, int in_h, int in_w, int
  *   out_dtype BF16 / F32 (res != NULL: C += ..., in place, f32) or MXFP8 (act must be 1 = bias +
  *   GELU-tanh, C e4m3 [M, N] + c_scales, N % 128 == 0). */
 size_t vcap_mx_scale_bytes(int rows, int K);
+/* bf16 qkv [frames*tokens, 3*heads*64] -> attention output in MXFP8 ([frames*tokens, heads*64] e4m3 +
+ * scales), the A operand of an MXFP8 attn-proj GEMM */
+int vcap_vit_attention_mx(const void* qkv, void* out, uint8_t* out_scales, int frames, int tokens, int heads,
+                          void* stream);
 int vcap_mx_quantize(int in_dtype, const void* x, int64_t ldx, int rows, int K, void* q, uint8_t* scales,
                      void* stream);
 int vcap_layernorm_mx(const float* x, int64_t ldx, void* q, uint8_t* scales, const float* gamma, const float* beta,

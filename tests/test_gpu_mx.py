@@ -159,3 +159,29 @@ def test_encoder_fp8_close_to_reference(device, name, tol):
     cos = (got * ref).sum(1) / np.linalg.norm(got, axis=1) / np.linalg.norm(ref, axis=1)
     print(f"{name}: fp8 encoder max|err| {err:.4f} (ref max {np.abs(ref).max():.3f}), min cos {cos.min():.6f}")
     assert err < tol and cos.min() > 0.995, (err, cos.min())
+
+
+@pytest.mark.parametrize("tokens,heads", [(197, 12), (257, 16)])
+def test_attention_mx_output(device, tokens, heads):
+    """MXFP8 attention output vs the bf16 attention output of the same kernel arithmetic: every
+    element within half an e4m3 step of the bf16 value (+ the bf16 rounding), scales equal except
+    where the bf16 rounding lifts a block max across a power of two."""
+    frames, D = 6, heads * 64
+    g = torch.Generator(device=device).manual_seed(0)
+    qkv = (torch.randn(frames * tokens, 3 * D, generator=g, device=device) * 1.5).bfloat16()
+    ref = torch.empty(frames * tokens, D, dtype=torch.bfloat16, device=device)
+    N.check(N.lib().vcap_vit_attention(N.DT_BF16, qkv.data_ptr(), ref.data_ptr(), frames, tokens, heads, _s()), "attn")
+    M = frames * tokens
+    q = torch.empty(M, D, dtype=torch.uint8, device=device)
+    sc = torch.zeros(int(N.lib().vcap_mx_scale_bytes(M, D)), dtype=torch.uint8, device=device)
+    N.check(N.lib().vcap_vit_attention_mx(qkv.data_ptr(), q.data_ptr(), sc.data_ptr(), frames, tokens, heads, _s()),
+            "attn mx")
+    torch.cuda.synchronize()
+    r = ref.float().cpu().numpy().astype(np.float64)
+    qo, so = O.mx_quantize(ref.float().cpu().numpy())
+    sg = O.mx_unpack_scales(sc.cpu().numpy(), M, D)
+    # a block max just below a power of two can round up to it in bf16: the scale then differs by 1
+    assert (sg == so).mean() > 0.99 and (np.abs(sg.astype(int) - so.astype(int)) <= 1).all()
+    got = O.mx_dequantize(q.cpu().numpy(), sg)
+    half_step = np.repeat(_e4m3_step(sg) / 2, 32, axis=1)
+    assert (np.abs(got - r) <= half_step + np.abs(r) * 2.0 ** -8 + 1e-12).all()

@@ -135,7 +135,7 @@ int check_vit(const vcap_vit_desc* d) {
   if (d->dtype == VCAP_DT_MXFP8) {
     if (d->dim > 1024) return fail(VCAP_E_UNSUPPORTED, "MXFP8 LayerNorm holds rows of <= 1024 in registers");
     for (int l = 0; l < d->depth; ++l)
-      if (!d->layers[l].qkv_ws || !d->layers[l].fc1_ws || !d->layers[l].fc2_ws)
+      if (!d->layers[l].qkv_ws || !d->layers[l].proj_ws || !d->layers[l].fc1_ws || !d->layers[l].fc2_ws)
         return fail(VCAP_E_ARG, "MXFP8 vit layer without weight scales");
   }
   if (d->image % d->patch) return fail(VCAP_E_ARG, "image not divisible by patch");
@@ -481,6 +481,17 @@ int vcap_vit_attention(int dtype, const void* qkv, void* out, int frames, int to
   return 0;
 }
 
+int vcap_vit_attention_mx(const void* qkv, void* out, uint8_t* out_scales, int frames, int tokens, int heads,
+                          void* stream) {
+  if (!qkv || !out || !out_scales || frames <= 0 || tokens <= 0 || heads <= 0)
+    return fail(VCAP_E_ARG, "vcap_vit_attention_mx: bad arguments");
+  if (tokens > 288) return fail(VCAP_E_UNSUPPORTED, "vcap_vit_attention_mx: tokens > 288");
+  if ((heads * 64) % 256) return fail(VCAP_E_UNSUPPORTED, "vcap_vit_attention_mx: heads*64 must be a multiple of 256");
+  VCAP_TRY(vcap_vit_attention_mx_dispatch(qkv, out, out_scales, frames, tokens, heads, (hipStream_t)stream),
+           "vcap_vit_attention_mx");
+  return 0;
+}
+
 int vcap_vit_pool_temporal(int dtype, const void* feat, void* out, int bsz, int timesteps, int tokens, int channels,
                            int pool_gap, void* stream) {
   if (!feat || !out || bsz <= 0 || timesteps <= 0 || tokens <= 0 || channels <= 0)
@@ -543,12 +554,18 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
     }
     {
       ProbeScope ps("vit.attention", s);
-      VCAP_TRY(vcap_vit_attention_dispatch(adt, w.qkv, w.attn, BT, N, d->heads, s), "attention");
+      if (mx)
+        VCAP_TRY(vcap_vit_attention_mx_dispatch(w.qkv, w.attn, w.xn_s, BT, N, d->heads, s), "attention");
+      else
+        VCAP_TRY(vcap_vit_attention_dispatch(adt, w.qkv, w.attn, BT, N, d->heads, s), "attention");
     }
-    GemmEpi e2{ly.proj_b, w.x, D, 0, 1, 0, 0, 0, 0};
+    // MXFP8: the attention output arrives as MXFP8 (its scales reuse xn_s, free until norm2)
+    GemmEpi e2{ly.proj_b, w.x, D, 0, 1, 0, 0, 0, 0, w.xn_s, ly.proj_ws, nullptr};
     {
       ProbeScope ps("vit.proj", s);
-      VCAP_TRY(vcap_gemm_dispatch(adt, VCAP_DT_F32, w.attn, D, ly.proj_w, D, w.x, D, M, D, D, e2, s), "attn_proj");
+      VCAP_TRY(vcap_gemm_dispatch(dt == VCAP_DT_MXFP8 ? dt : adt, VCAP_DT_F32, w.attn, D, ly.proj_w, D, w.x, D, M, D,
+                                  D, e2, s),
+               "attn_proj");
     }
     if (mx)
       VCAP_TRY(vcap_layernorm_mx_dispatch(w.x, D, (uint8_t*)w.xn, w.xn_s, M, ly.ln2_g, ly.ln2_b, M, D, d->ln_eps, s),

@@ -186,10 +186,13 @@ VCAP_DEV u32x2 tr_read(const char* p) {
 // One workgroup per (frame, head) pair; two of them share a CU (56 KiB of LDS, <= 128 VGPRs
 // for 4 waves per SIMD), so one pair's DMA overlaps the other's MFMA / softmax.  (A persistent
 // double-buffered variant measured slower: its doubled Q registers cost half the occupancy.)
-template <int KT, int WAVES>
+// MXO: write the output as MXFP8 (e4m3 + E8M0 per 32 of the head's 64 dims) for an MXFP8 attn-proj
+// GEMM; oscale in the vcap_common.h layout over `groups` 256-row groups.
+template <int KT, int WAVES, bool MXO>
 __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(const bf16_t* __restrict__ qkv,
-                                                                             bf16_t* __restrict__ out, int N,
-                                                                             int H) {
+                                                                             void* __restrict__ out, int N, int H,
+                                                                             uint8_t* __restrict__ oscale,
+                                                                             int groups) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NP = KT * 16;
   constexpr int QT_MAX = (KT + WAVES - 1) / WAVES;  // query tiles per wave (N <= NP)
@@ -288,9 +291,28 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
       }
     }
     const int q = qt * 16 + fr;
-    if (q < N) {
-      const float inv = 1.0f / sum;
-      bf16_t* orow = out + ((long)bt * N + q) * D + h * 64;
+    const float inv = 1.0f / sum;
+    if constexpr (MXO) {
+      // block b = dims [32b, 32b+32) of row q: dt in {2b, 2b+1} of this lane and lanes fg = 0..3
+      const long row = (long)bt * N + q;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const f32x4 v0 = o[2 * b] * inv, v1 = o[2 * b + 1] * inv;
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fmaxf(fabsf(v0[e]), fabsf(v1[e])));
+        amax = rows_max(amax);
+        const int sb = mx_scale_byte(amax);
+        const float is = mx_inv_scale(sb);
+        if (q < N) {
+          uint8_t* orow = (uint8_t*)out + row * D + h * 64 + 32 * b;
+          *reinterpret_cast<uint32_t*>(orow + 4 * fg) = pack_fp8x4(v0.x * is, v0.y * is, v0.z * is, v0.w * is);
+          *reinterpret_cast<uint32_t*>(orow + 16 + 4 * fg) = pack_fp8x4(v1.x * is, v1.y * is, v1.z * is, v1.w * is);
+          if (fg == 0) oscale[mx_scale_index((int)row, h * 64 + 32 * b, groups)] = (uint8_t)sb;
+        }
+      }
+    } else if (q < N) {
+      bf16_t* orow = (bf16_t*)out + ((long)bt * N + q) * D + h * 64;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const f32x4 v = o[dt] * inv;  // O[q][d = dt*16 + 4*fg + r]
@@ -300,18 +322,19 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
   }
 }
 
-template <int KT, int WAVES>
-static hipError_t launch_attn_bf16(const void* qkv, void* out, int BT, int N, int H, hipStream_t s) {
+template <int KT, int WAVES, bool MXO>
+static hipError_t launch_attn_bf16(const void* qkv, void* out, int BT, int N, int H, uint8_t* oscale, hipStream_t s) {
   const size_t lds = (size_t)KT * 16 * 128 * 2;
   static bool configured = false;
   if (!configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_bf16_kernel<KT, WAVES>,
+    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_bf16_kernel<KT, WAVES, MXO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     configured = true;
   }
-  hipLaunchKernelGGL((vcap_vit_attention_bf16_kernel<KT, WAVES>), dim3(BT * H), dim3(WAVES * 64), lds, s,
-                     (const bf16_t*)qkv, (bf16_t*)out, N, H);
+  const int groups = (BT * N + 255) / 256;
+  hipLaunchKernelGGL((vcap_vit_attention_bf16_kernel<KT, WAVES, MXO>), dim3(BT * H), dim3(WAVES * 64), lds, s,
+                     (const bf16_t*)qkv, out, N, H, oscale, groups);
   return hipGetLastError();
 }
 
@@ -337,9 +360,9 @@ hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int B
   const int kt = ((N + 31) / 32) * 2;  // keys padded to a multiple of 32
   if (dt == VCAP_DT_BF16) {
     switch (kt) {
-      case 2: return launch_attn_bf16<2, 4>(qkv, out, BT, N, H, s);
-      case 14: return launch_attn_bf16<14, 8>(qkv, out, BT, N, H, s);
-      case 18: return launch_attn_bf16<18, 8>(qkv, out, BT, N, H, s);
+      case 2: return launch_attn_bf16<2, 4, false>(qkv, out, BT, N, H, nullptr, s);
+      case 14: return launch_attn_bf16<14, 8, false>(qkv, out, BT, N, H, nullptr, s);
+      case 18: return launch_attn_bf16<18, 8, false>(qkv, out, BT, N, H, nullptr, s);
       default: return hipErrorInvalidValue;
     }
   }
@@ -347,6 +370,18 @@ hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int B
     case 2: return launch_attn<float, 2>(qkv, out, BT, N, H, s);
     case 14: return launch_attn<float, 14>(qkv, out, BT, N, H, s);
     case 18: return launch_attn<float, 18>(qkv, out, BT, N, H, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// bf16 q/k/v -> MXFP8 attention output (+ scales) for the MXFP8 attn-proj GEMM
+hipError_t vcap_vit_attention_mx_dispatch(const void* qkv, void* out, uint8_t* oscale, int BT, int N, int H,
+                                          hipStream_t s) {
+  if (N <= 0 || N > 288 || !oscale) return hipErrorInvalidValue;
+  switch (((N + 31) / 32) * 2) {
+    case 2: return launch_attn_bf16<2, 4, true>(qkv, out, BT, N, H, oscale, s);
+    case 14: return launch_attn_bf16<14, 8, true>(qkv, out, BT, N, H, oscale, s);
+    case 18: return launch_attn_bf16<18, 8, true>(qkv, out, BT, N, H, oscale, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -16,7 +16,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
 DT_F32, DT_BF16, DT_MXFP8 = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
@@ -29,7 +29,7 @@ class VcapError(RuntimeError):
 class VitLayer(C.Structure):
     _fields_ = [("ln1_g", vp), ("ln1_b", vp), ("qkv_w", vp), ("qkv_b", vp), ("proj_w", vp), ("proj_b", vp),
                 ("ln2_g", vp), ("ln2_b", vp), ("fc1_w", vp), ("fc1_b", vp), ("fc2_w", vp), ("fc2_b", vp),
-                ("qkv_ws", vp), ("fc1_ws", vp), ("fc2_ws", vp)]
+                ("qkv_ws", vp), ("proj_ws", vp), ("fc1_ws", vp), ("fc2_ws", vp)]
 
 
 class VitDesc(C.Structure):
@@ -77,6 +77,7 @@ SIGNATURES = {
     "vcap_frames_workspace_bytes": (sz, [i32, i32, i32, i32, i32]),
     "vcap_frames_preprocess": (i32, [vp, i32, i32, i32, i32, i32, fp, fp, vp, vp, vp, sz, vp]),
     "vcap_mx_scale_bytes": (sz, [i32, i32]),
+    "vcap_vit_attention_mx": (i32, [vp, vp, vp, i32, i32, i32, vp]),
     "vcap_mx_quantize": (i32, [i32, vp, i64, i32, i32, vp, vp, vp]),
     "vcap_layernorm_mx": (i32, [vp, i64, vp, vp, vp, vp, i32, i32, f32, vp]),
     "vcap_gemm_mx": (i32, [vp, vp, vp, vp, i32, vp, i64, vp, i32, i32, i32, vp, i32, vp, vp]),

@@ -24,8 +24,8 @@ from . import _native as N
 from .configs import VIDEO_DIM, GPT2Arch, ViTArch
 
 _DTYPES = {"bf16": (N.DT_BF16, torch.bfloat16), "fp32": (N.DT_F32, torch.float32)}
-# ViT only: "fp8" = MXFP8 block GEMMs (QKV / fc1 / fc2: e4m3 + E8M0 per 32 K elements, the gfx950
-# scaled-MFMA format; BASELINE configs[4]); patch-embed, attention and attn-proj run in bf16.
+# ViT only: "fp8" = MXFP8 block GEMMs (QKV / attn-proj / fc1 / fc2: e4m3 + E8M0 per 32 K elements,
+# the gfx950 scaled-MFMA format; BASELINE configs[4]); patch-embed and QK^T / PV run in bf16.
 _VIT_DTYPES = dict(_DTYPES, fp8=(N.DT_MXFP8, torch.bfloat16))
 
 
@@ -106,11 +106,11 @@ class HipViTEncoder:
         for i in range(arch.depth):
             b = f"{p}blocks.{i}."
             lt = dict(ln1_g=f32(b + "norm1.weight"), ln1_b=f32(b + "norm1.bias"),
-                      qkv_b=f32(b + "attn.qkv.bias"),
-                      proj_w=wt(b + "attn.proj.weight"), proj_b=f32(b + "attn.proj.bias"),
+                      qkv_b=f32(b + "attn.qkv.bias"), proj_b=f32(b + "attn.proj.bias"),
                       ln2_g=f32(b + "norm2.weight"), ln2_b=f32(b + "norm2.bias"),
                       fc1_b=f32(b + "mlp.fc1.bias"), fc2_b=f32(b + "mlp.fc2.bias"))
-            for name, key in (("qkv", "attn.qkv.weight"), ("fc1", "mlp.fc1.weight"), ("fc2", "mlp.fc2.weight")):
+            for name, key in (("qkv", "attn.qkv.weight"), ("proj", "attn.proj.weight"), ("fc1", "mlp.fc1.weight"),
+                              ("fc2", "mlp.fc2.weight")):
                 if mx:
                     lt[name + "_w"], lt[name + "_ws"] = wmx(b + key)
                 else:

@@ -9,6 +9,7 @@ candidates (the reference re-runs the ViT per candidate, core/engine.py:43; resu
 from __future__ import annotations
 
 import logging
+from typing import List, Sequence
 
 import torch
 
@@ -70,3 +71,40 @@ class InferenceEngine:
         )
         key, text, _ = select_best([("S1", cands.s1), ("S2", cands.s2), ("S3", cands.s3)])
         return InferenceResult(candidates=cands, best_key=key, best_text=text)
+
+    def _decode_rows(self, prefix: torch.Tensor, prompt: str, **decode_kwargs) -> List[str]:
+        """_decode for every row of a batched prefix: greedy rows and beam hypotheses evolve per
+        sequence, so each row's caption equals its single-video decode (sampling draws from one
+        generator for the whole batch: distributional parity only, as for single videos)."""
+        dec = self.model.decoder
+        rows = dec.generate_from_prefix(
+            prefix, dec.tokenizer.encode_prompt(prompt or ""),
+            max_new_tokens=decode_kwargs.get("max_new_tokens", 24), num_beams=decode_kwargs.get("num_beams", 3),
+            temperature=decode_kwargs.get("temperature", 1.0), top_p=decode_kwargs.get("top_p", 1.0),
+            no_repeat_ngram_size=decode_kwargs.get("no_repeat_ngram_size", 3),
+            repetition_penalty=decode_kwargs.get("repetition_penalty", 1.1), min_new_tokens=8,
+            seed=self.config.sample_seed)
+        return [clean_text(t.strip()) for t in dec.tokenizer.batch_decode(rows, skip_special_tokens=True)]
+
+    @torch.no_grad()
+    def infer_videos(self, videos: torch.Tensor) -> List[InferenceResult]:
+        """infer_video over a batch [B, T, 3, H, W]: ONE fused encode for all B videos and one
+        batched decode per candidate (the serving path coalesces requests into this call)."""
+        prefix = self._prefix(videos)
+        c = self.config
+        s1 = self._decode_rows(prefix, c.prompt1, **preset_to_kwargs(c.preset1))
+        s2 = self._decode_rows(prefix, c.prompt2, **preset_to_kwargs(c.preset2))
+        s3 = self._decode_rows(prefix, c.prompt3, **preset_to_kwargs(c.preset3))
+        out = []
+        for a, b, d in zip(s1, s2, s3):
+            key, text, _ = select_best([("S1", a), ("S2", b), ("S3", d)])
+            out.append(InferenceResult(candidates=CaptionCandidates(s1=a, s2=b, s3=d), best_key=key, best_text=text))
+        return out
+
+    @torch.no_grad()
+    def infer_batch(self, frames_dirs: Sequence[str]) -> List[InferenceResult]:
+        """infer() for several frames directories in one engine call (each video's frames share a
+        size; videos are preprocessed on the GPU one by one and encoded/decoded together)."""
+        vids = [load_video_tensor(d, num_frames=self.config.num_frames, image_size=self.config.image_size,
+                                  device=self.device) for d in frames_dirs]
+        return self.infer_videos(torch.cat(vids, dim=0))

@@ -48,5 +48,10 @@ for _h in (
     PluginHook("vit_encoder", "src.models.video_encoder.ViTFrameEncoder", "HipViTEncode", "vcap_vit_encode"),
     PluginHook("gpt2_generate", "src.models.text_decoder.GPT2TextDecoder.generate", "HipGPT2Generate",
                "vcap_gpt2_generate"),
+    PluginHook("frame_transform", "core.preprocessing.frame_loader (torchvision Resize/ToTensor/Normalize)",
+               "HipFrameTransform", "vcap_frames_preprocess"),
+    PluginHook("vit_linear_fp8", "timm Linear (qkv / proj / fc1 / fc2) in MXFP8", "HipMXFP8Linear", "vcap_gemm_mx"),
+    PluginHook("vit_layernorm_fp8", "timm LayerNorm feeding an MXFP8 GEMM", "HipMXFP8LayerNorm",
+               "vcap_layernorm_mx"),
 ):
     register_plugin_hook(_h)

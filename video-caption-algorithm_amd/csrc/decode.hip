@@ -817,10 +817,89 @@ size_t vcap_rows_packed_size(int dt, int N, int K) {
   return (size_t)((N + 15) / 16) * (size_t)(K / ks) * 1024;
 }
 
+// bf16 fast path for contexts of at most 64 positions with the contiguous page layout the
+// runtime allocates (page of position j of sequence `seq` = seq * maxp + j / 16, i.e. the identity
+// page table): page ids are computed, not loaded, and q, the lane's K row and all of its V rows
+// are issued together, so the wave pays ONE memory round trip instead of three
+// (page table -> K -> V).  Arithmetic identical to vcap_decode_attention_kernel.
+__global__ __launch_bounds__(256) void vcap_decode_attention_c64_kernel(const bf16_t* __restrict__ q,
+                                                                        const bf16_t* __restrict__ kc,
+                                                                        const bf16_t* __restrict__ vc, int maxp,
+                                                                        bf16_t* __restrict__ out, int M, int H,
+                                                                        int S_new, int past) {
+  __shared__ float s_q[4][64];
+  __shared__ float s_p[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int item = blockIdx.x * 4 + wave;
+  if (item >= M * H) return;
+  const int m = item / H, h = item - m * H;
+  const int E = H * 64;
+  const int seq = m / S_new, qpos = past + (m - seq * S_new);
+  const int ctx = qpos + 1;  // <= 64 (dispatcher)
+  auto row_of = [&](const bf16_t* pool, int j) {
+    return pool + (((long)(seq * maxp + (j >> 4)) * H + h) * 16 + (j & 15)) * 64;
+  };
+  const float qv = bf2f(q[(long)m * E + h * 64 + lane]);
+  const bf16_t* krow = row_of(kc, min(lane, ctx - 1));
+  u32x4 kv[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) kv[c] = *reinterpret_cast<const u32x4*>(krow + c * 8);
+  const int kg = lane >> 3, d8 = (lane & 7) * 8;
+  u32x4 vv[8];
+#pragma unroll
+  for (int it = 0; it < 8; ++it)
+    vv[it] = *reinterpret_cast<const u32x4*>(row_of(vc, min(it * 8 + kg, ctx - 1)) + d8);
+  s_q[wave][lane] = qv;
+  __builtin_amdgcn_wave_barrier();
+  float sc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const bf16_t* ke = reinterpret_cast<const bf16_t*>(&kv[c]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sc += s_q[wave][c * 8 + e] * bf2f(ke[e]);
+  }
+  sc *= 0.125f;
+  const bool live = lane < ctx;
+  const float mx = wave_max(live ? sc : -INFINITY);
+  const float p = live ? __expf(sc - mx) : 0.f;
+  const float sum = wave_sum(p);
+  s_p[wave][lane] = p;
+  __builtin_amdgcn_wave_barrier();
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = 0.f;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int jj = it * 8 + kg;
+    const float pj = jj < ctx ? s_p[wave][jj] : 0.f;
+    const unsigned w4[4] = {vv[it].x, vv[it].y, vv[it].z, vv[it].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[2 * e] += pj * bf2f((bf16_t)(w4[e] & 0xffff));
+      o[2 * e + 1] += pj * bf2f((bf16_t)(w4[e] >> 16));
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = rows_sum(o[e] + dpp_f<0x128>(o[e]));
+  if (kg == 0) {
+    const float inv = 1.0f / sum;
+    bf16_t* orow = out + (long)m * E + h * 64 + d8;
+    *reinterpret_cast<u32x4*>(orow) =
+        (u32x4){pack_bf2(o[0] * inv, o[1] * inv), pack_bf2(o[2] * inv, o[3] * inv),
+                pack_bf2(o[4] * inv, o[5] * inv), pack_bf2(o[6] * inv, o[7] * inv)};
+  }
+}
+
 hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc, const void* vc, const int* pt,
                                           int maxp, void* out, int M, int H, int S_new, int past, hipStream_t s) {
   if (past + S_new > 1024 || maxp > 64) return hipErrorInvalidValue;
   const dim3 grid((M * H + 3) / 4), block(256);
+  if (dt == VCAP_DT_BF16 && !pt && past + S_new <= 64) {
+    hipLaunchKernelGGL(vcap_decode_attention_c64_kernel, grid, block, 0, s, (const bf16_t*)q, (const bf16_t*)kc,
+                       (const bf16_t*)vc, maxp, (bf16_t*)out, M, H, S_new, past);
+    return hipGetLastError();
+  }
+  if (!pt) return hipErrorInvalidValue;  // the general kernels read the page table
   if (dt == VCAP_DT_BF16)
     hipLaunchKernelGGL((vcap_decode_attention_kernel<bf16_t>), grid, block, 0, s, (const bf16_t*)q,
                        (const bf16_t*)kc, (const bf16_t*)vc, pt, maxp, (bf16_t*)out, M, H, S_new, past);

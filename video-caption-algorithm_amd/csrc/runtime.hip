@@ -227,7 +227,10 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     a.page_table = w.pt; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past; a.max_blocks = max_blocks;
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
     // 2) causal attention over the paged cache
-    VCAP_TRY(vcap_decode_attention_dispatch(dt, w.q, a.kc, a.vc, w.pt, maxp, w.attn, M, H, S_new, past, s),
+    // pages are allocated contiguously per sequence (vcap_decode_init: identity table), so the bf16
+    // short-context kernel computes page ids instead of loading them (nullptr table)
+    const int* pt_arg = (dt == VCAP_DT_BF16 && past + S_new <= 64) ? nullptr : w.pt;
+    VCAP_TRY(vcap_decode_attention_dispatch(dt, w.q, a.kc, a.vc, pt_arg, maxp, w.attn, M, H, S_new, past, s),
              "decode_attention");
     // 3) attn c_proj + residual
     RowsGemmArgs b;

@@ -219,6 +219,7 @@ def main():
                           "achieved_tflops": attn_flops / attn_avg_s / 1e12,
                           "frac_of_peak": attn_flops / attn_avg_s / 1e12 / peak},
             "vit_flops_per_step": B * T * va.flops_per_frame(),
+            "vit_flops_per_step_executed": B * T * va.flops_per_frame(cls_tail=True),
         }
         if world == 1 and args.cpu_baseline_s > 0:
             out["cpu_baseline"] = cpu_baseline(sd, va, ga, frames_np, args.cpu_baseline_s, args.max_new)

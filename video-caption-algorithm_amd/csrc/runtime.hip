@@ -545,6 +545,14 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
            "patch_gemm");
   for (int l = 0; l < d->depth; ++l) {
     const vcap_vit_layer& ly = d->layers[l];
+    // The last block feeds only the class-token rows (final LN on CLS rows, CLS temporal pool:
+    // video_encoder.py:256-258, pool="cls" at caption_model.py:45), so after its QKV projection
+    // (K/V of every token are needed) it runs on the BT CLS rows only: CLS-query attention into a
+    // compact [BT, D] buffer, then attn-proj / LN2 / fc1 / fc2 on BT rows with the residual rows
+    // remapped to x[bt*N] (GemmEpi G = 1, Gs = N).  Outputs are identical; 6 % fewer FLOPs.
+    const bool last = l == d->depth - 1;
+    const int Mt = last ? BT : M;                       // rows after the QKV projection
+    const char* probe_attn = last ? "vit.attention.cls" : "vit.attention";
     if (mx)
       VCAP_TRY(vcap_layernorm_mx_dispatch(w.x, D, (uint8_t*)w.xn, w.xn_s, M, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s),
                "norm1");
@@ -556,34 +564,37 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
       VCAP_TRY(vcap_gemm_dispatch(dt, adt, w.xn, D, ly.qkv_w, D, w.qkv, 3 * D, M, 3 * D, D, e1, s), "qkv");
     }
     {
-      ProbeScope ps("vit.attention", s);
+      ProbeScope ps(probe_attn, s);
       if (mx)
-        VCAP_TRY(vcap_vit_attention_mx_dispatch(w.qkv, w.attn, w.xn_s, BT, N, d->heads, s), "attention");
+        VCAP_TRY(vcap_vit_attention_mx_dispatch(w.qkv, w.attn, w.xn_s, BT, N, d->heads, s, last), "attention");
       else
-        VCAP_TRY(vcap_vit_attention_dispatch(adt, w.qkv, w.attn, BT, N, d->heads, s), "attention");
+        VCAP_TRY(vcap_vit_attention_dispatch(adt, w.qkv, w.attn, BT, N, d->heads, s, last), "attention");
     }
     // MXFP8: the attention output arrives as MXFP8 (its scales reuse xn_s, free until norm2)
-    GemmEpi e2{ly.proj_b, w.x, D, 0, 1, 0, 0, 0, 0, w.xn_s, ly.proj_ws, nullptr};
+    GemmEpi e2{ly.proj_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, w.xn_s, ly.proj_ws, nullptr};
     {
-      ProbeScope ps("vit.proj", s);
-      VCAP_TRY(vcap_gemm_dispatch(dt == VCAP_DT_MXFP8 ? dt : adt, VCAP_DT_F32, w.attn, D, ly.proj_w, D, w.x, D, M, D,
+      ProbeScope ps(last ? "vit.proj.cls" : "vit.proj", s);
+      VCAP_TRY(vcap_gemm_dispatch(dt == VCAP_DT_MXFP8 ? dt : adt, VCAP_DT_F32, w.attn, D, ly.proj_w, D, w.x, D, Mt, D,
                                   D, e2, s),
                "attn_proj");
     }
+    const long ldx2 = last ? (long)N * D : D;            // CLS rows of x are N*D apart
     if (mx)
-      VCAP_TRY(vcap_layernorm_mx_dispatch(w.x, D, (uint8_t*)w.xn, w.xn_s, M, ly.ln2_g, ly.ln2_b, M, D, d->ln_eps, s),
+      VCAP_TRY(vcap_layernorm_mx_dispatch(w.x, ldx2, (uint8_t*)w.xn, w.xn_s, Mt, ly.ln2_g, ly.ln2_b, Mt, D,
+                                          d->ln_eps, s),
                "norm2");
     else
-      VCAP_TRY(vcap_layernorm_dispatch(dt, w.x, D, w.xn, D, ly.ln2_g, ly.ln2_b, M, D, d->ln_eps, s), "norm2");
+      VCAP_TRY(vcap_layernorm_dispatch(dt, w.x, ldx2, w.xn, D, ly.ln2_g, ly.ln2_b, Mt, D, d->ln_eps, s), "norm2");
     GemmEpi e3{ly.fc1_b, nullptr, 0, 1, 0, 0, 0, 0, 0, w.xn_s, ly.fc1_ws, w.act_s};
     {
-      ProbeScope ps("vit.fc1", s);
-      VCAP_TRY(vcap_gemm_dispatch(dt, dt, w.xn, D, ly.fc1_w, D, w.act, d->mlp, M, d->mlp, D, e3, s), "fc1");
+      ProbeScope ps(last ? "vit.fc1.cls" : "vit.fc1", s);
+      VCAP_TRY(vcap_gemm_dispatch(dt, dt, w.xn, D, ly.fc1_w, D, w.act, d->mlp, Mt, d->mlp, D, e3, s), "fc1");
     }
-    GemmEpi e4{ly.fc2_b, w.x, D, 0, 1, 0, 0, 0, 0, w.act_s, ly.fc2_ws, nullptr};
+    GemmEpi e4{ly.fc2_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, w.act_s, ly.fc2_ws, nullptr};
     {
-      ProbeScope ps("vit.fc2", s);
-      VCAP_TRY(vcap_gemm_dispatch(dt, VCAP_DT_F32, w.act, d->mlp, ly.fc2_w, d->mlp, w.x, D, M, D, d->mlp, e4, s), "fc2");
+      ProbeScope ps(last ? "vit.fc2.cls" : "vit.fc2", s);
+      VCAP_TRY(vcap_gemm_dispatch(dt, VCAP_DT_F32, w.act, d->mlp, ly.fc2_w, d->mlp, w.x, D, Mt, D, d->mlp, e4, s),
+               "fc2");
     }
   }
   const float ls = pd ? pd->ln_scale : 0.f, iw = pd ? pd->in_weight : 0.f;

@@ -65,9 +65,11 @@ hipError_t vcap_mx_quantize_dispatch(int in_dt, const void* x, long ldx, int row
                                      uint8_t* scales, int srows, hipStream_t s);
 hipError_t vcap_layernorm_dispatch(int out_dt, const float* x, long ldx, void* y, long ldy, const float* gamma,
                                    const float* beta, int rows, int D, float eps, hipStream_t s);
-hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s);
+// cls_only: only the class-token query of each (frame, head), written to compact row `frame`
+hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s,
+                                       int cls_only = 0);
 hipError_t vcap_vit_attention_mx_dispatch(const void* qkv, void* out, uint8_t* oscale, int BT, int N, int H,
-                                          hipStream_t s);
+                                          hipStream_t s, int cls_only = 0);
 hipError_t vcap_patchify_dispatch(int dt, const float* frames, void* patches, float* x, const float* cls,
                                   const float* pos, int BT, int img, int p, int Kp, int N, int D, hipStream_t s);
 hipError_t vcap_vit_head_prefix_dispatch(const float* x, int B, int T, int N, int D, const float* ng, const float* nb,

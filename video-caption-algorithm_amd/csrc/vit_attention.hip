@@ -14,9 +14,11 @@
 #include "vcap_common.h"
 #include "vcap_kernels.h"
 
+// cls_only: compute the class-token query (q = 0) of each (frame, head) only and write it to
+// compact row `frame` of out (the last block of the encoder: only CLS rows are consumed after it).
 template <typename T, int KT>
 __global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __restrict__ qkv, T* __restrict__ out,
-                                                                 int N, int H) {
+                                                                 int N, int H, int cls_only) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int E = Frag<T>::kElems;     // elements per 16-byte chunk
   constexpr int CH = 64 / E;             // chunks per 64-dim row (8 bf16, 16 f32)
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __rest
   __syncthreads();
 
   const int fr = lane & 15, fg = lane >> 4;
-  const int qtiles = (N + 15) / 16;
+  const int qtiles = cls_only ? 1 : (N + 15) / 16;
   const float scale = 0.125f;  // 64^-0.5
   for (int qt = wave; qt < qtiles; qt += 4) {
     int q = qt * 16 + fr;
@@ -138,8 +140,8 @@ __global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __rest
         }
       }
     }
-    if (q < N) {
-      T* orow = out + ((long)bt * N + q) * D + h * 64;
+    if (q < N && (!cls_only || q == 0)) {
+      T* orow = out + (cls_only ? (long)bt : (long)bt * N + q) * D + h * 64;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const f32x4 v = o[dt] * inv;  // O^T[d = dt*16 + 4*fg + r][q]
@@ -192,7 +194,7 @@ template <int KT, int WAVES, bool MXO>
 __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(const bf16_t* __restrict__ qkv,
                                                                              void* __restrict__ out, int N, int H,
                                                                              uint8_t* __restrict__ oscale,
-                                                                             int groups) {
+                                                                             int groups, int cls_only) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NP = KT * 16;
   constexpr int QT_MAX = (KT + WAVES - 1) / WAVES;  // query tiles per wave (N <= NP)
@@ -218,7 +220,7 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
     glds16_attn(src + 2 * D, Vs + blk * 1024);
   }
   // ---- this wave's Q fragments
-  const int qtiles = (N + 15) / 16;
+  const int qtiles = cls_only ? 1 : (N + 15) / 16;
   u32x4 qf[QT_MAX][2];
 #pragma unroll
   for (int i = 0; i < QT_MAX; ++i) {
@@ -292,9 +294,10 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
     }
     const int q = qt * 16 + fr;
     const float inv = 1.0f / sum;
+    const bool keep = q < N && (!cls_only || q == 0);
+    const long row = cls_only ? (long)bt : (long)bt * N + q;
     if constexpr (MXO) {
       // block b = dims [32b, 32b+32) of row q: dt in {2b, 2b+1} of this lane and lanes fg = 0..3
-      const long row = (long)bt * N + q;
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const f32x4 v0 = o[2 * b] * inv, v1 = o[2 * b + 1] * inv;
@@ -304,15 +307,15 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
         amax = rows_max(amax);
         const int sb = mx_scale_byte(amax);
         const float is = mx_inv_scale(sb);
-        if (q < N) {
+        if (keep) {
           uint8_t* orow = (uint8_t*)out + row * D + h * 64 + 32 * b;
           *reinterpret_cast<uint32_t*>(orow + 4 * fg) = pack_fp8x4(v0.x * is, v0.y * is, v0.z * is, v0.w * is);
           *reinterpret_cast<uint32_t*>(orow + 16 + 4 * fg) = pack_fp8x4(v1.x * is, v1.y * is, v1.z * is, v1.w * is);
           if (fg == 0) oscale[mx_scale_index((int)row, h * 64 + 32 * b, groups)] = (uint8_t)sb;
         }
       }
-    } else if (q < N) {
-      bf16_t* orow = (bf16_t*)out + ((long)bt * N + q) * D + h * 64;
+    } else if (keep) {
+      bf16_t* orow = (bf16_t*)out + row * D + h * 64;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const f32x4 v = o[dt] * inv;  // O[q][d = dt*16 + 4*fg + r]
@@ -323,7 +326,8 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
 }
 
 template <int KT, int WAVES, bool MXO>
-static hipError_t launch_attn_bf16(const void* qkv, void* out, int BT, int N, int H, uint8_t* oscale, hipStream_t s) {
+static hipError_t launch_attn_bf16(const void* qkv, void* out, int BT, int N, int H, uint8_t* oscale, int cls_only,
+                                   hipStream_t s) {
   const size_t lds = (size_t)KT * 16 * 128 * 2;
   static bool configured = false;
   if (!configured) {
@@ -332,14 +336,14 @@ static hipError_t launch_attn_bf16(const void* qkv, void* out, int BT, int N, in
     if (e != hipSuccess) return e;
     configured = true;
   }
-  const int groups = (BT * N + 255) / 256;
+  const int groups = ((cls_only ? BT : BT * N) + 255) / 256;  // scale rows = output rows
   hipLaunchKernelGGL((vcap_vit_attention_bf16_kernel<KT, WAVES, MXO>), dim3(BT * H), dim3(WAVES * 64), lds, s,
-                     (const bf16_t*)qkv, out, N, H, oscale, groups);
+                     (const bf16_t*)qkv, out, N, H, oscale, groups, cls_only);
   return hipGetLastError();
 }
 
 template <typename T, int KT>
-static hipError_t launch_attn(const void* qkv, void* out, int BT, int N, int H, hipStream_t s) {
+static hipError_t launch_attn(const void* qkv, void* out, int BT, int N, int H, int cls_only, hipStream_t s) {
   constexpr int NP = KT * 16;
   constexpr int VS = NP + (sizeof(T) == 2 ? 8 : 4);
   const size_t lds = (size_t)NP * 64 * sizeof(T) + (size_t)64 * VS * sizeof(T);
@@ -351,37 +355,38 @@ static hipError_t launch_attn(const void* qkv, void* out, int BT, int N, int H, 
     configured = true;
   }
   hipLaunchKernelGGL((vcap_vit_attention_kernel<T, KT>), dim3(BT * H), dim3(256), lds, s, (const T*)qkv, (T*)out, N,
-                     H);
+                     H, cls_only);
   return hipGetLastError();
 }
 
-hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s) {
+hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s,
+                                       int cls_only) {
   if (N <= 0 || N > 288) return hipErrorInvalidValue;
   const int kt = ((N + 31) / 32) * 2;  // keys padded to a multiple of 32
   if (dt == VCAP_DT_BF16) {
     switch (kt) {
-      case 2: return launch_attn_bf16<2, 4, false>(qkv, out, BT, N, H, nullptr, s);
-      case 14: return launch_attn_bf16<14, 8, false>(qkv, out, BT, N, H, nullptr, s);
-      case 18: return launch_attn_bf16<18, 8, false>(qkv, out, BT, N, H, nullptr, s);
+      case 2: return launch_attn_bf16<2, 4, false>(qkv, out, BT, N, H, nullptr, cls_only, s);
+      case 14: return launch_attn_bf16<14, 8, false>(qkv, out, BT, N, H, nullptr, cls_only, s);
+      case 18: return launch_attn_bf16<18, 8, false>(qkv, out, BT, N, H, nullptr, cls_only, s);
       default: return hipErrorInvalidValue;
     }
   }
   switch (kt) {
-    case 2: return launch_attn<float, 2>(qkv, out, BT, N, H, s);
-    case 14: return launch_attn<float, 14>(qkv, out, BT, N, H, s);
-    case 18: return launch_attn<float, 18>(qkv, out, BT, N, H, s);
+    case 2: return launch_attn<float, 2>(qkv, out, BT, N, H, cls_only, s);
+    case 14: return launch_attn<float, 14>(qkv, out, BT, N, H, cls_only, s);
+    case 18: return launch_attn<float, 18>(qkv, out, BT, N, H, cls_only, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 // bf16 q/k/v -> MXFP8 attention output (+ scales) for the MXFP8 attn-proj GEMM
 hipError_t vcap_vit_attention_mx_dispatch(const void* qkv, void* out, uint8_t* oscale, int BT, int N, int H,
-                                          hipStream_t s) {
+                                          hipStream_t s, int cls_only) {
   if (N <= 0 || N > 288 || !oscale) return hipErrorInvalidValue;
   switch (((N + 31) / 32) * 2) {
-    case 2: return launch_attn_bf16<2, 4, true>(qkv, out, BT, N, H, oscale, s);
-    case 14: return launch_attn_bf16<14, 8, true>(qkv, out, BT, N, H, oscale, s);
-    case 18: return launch_attn_bf16<18, 8, true>(qkv, out, BT, N, H, oscale, s);
+    case 2: return launch_attn_bf16<2, 4, true>(qkv, out, BT, N, H, oscale, cls_only, s);
+    case 14: return launch_attn_bf16<14, 8, true>(qkv, out, BT, N, H, oscale, cls_only, s);
+    case 18: return launch_attn_bf16<18, 8, true>(qkv, out, BT, N, H, oscale, cls_only, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -45,11 +45,17 @@ class ViTArch:
     def patch_k(self) -> int:
         return 3 * self.patch * self.patch
 
-    def flops_per_frame(self) -> float:
-        """Algorithmic FLOPs per frame (full reference semantics)."""
+    def flops_per_frame(self, cls_tail: bool = False) -> float:
+        """Algorithmic FLOPs per frame (full reference semantics).  cls_tail: the last
+        block computed for the class-token row only after its QKV projection (the rows the encoder
+        output depends on; what vcap_vit_encode runs)."""
         n, d, m = self.tokens, self.dim, self.mlp
         per_block = 2 * n * d * 3 * d + 2 * 2 * n * n * d + 2 * n * d * d + 2 * 2 * n * d * m
-        return float(per_block * self.depth + 2 * self.num_patches * self.patch_k * d)
+        total = per_block * self.depth + 2 * self.num_patches * self.patch_k * d
+        if cls_tail:
+            tail = 2 * n * d * 3 * d + 2 * 2 * n * d + 2 * d * d + 2 * 2 * d * m
+            total += tail - per_block
+        return float(total)
 
 
 @dataclass(frozen=True)

@@ -72,7 +72,8 @@ VCAP_DEV void rows_epilogue(const RowsGemmArgs& a, int m0, const float (*red)[MT
         } else {
           const int head = within_e >> 6, d = within_e & 63;
           const int seq = m / a.S_new, pos = a.past + (m - seq * a.S_new);
-          const int page = a.page_table[seq * a.maxp + (pos >> 4)];
+          // contiguous per-sequence pages (identity table) unless an explicit table is given
+          const int page = a.page_table ? a.page_table[seq * a.maxp + (pos >> 4)] : seq * a.maxp + (pos >> 4);
           T* pool = (T*)(which == 1 ? a.kc : a.vc);
           pool[(((long)page * a.H + head) * 16 + (pos & 15)) * 64 + d] = Num<T>::from_f(v);
         }

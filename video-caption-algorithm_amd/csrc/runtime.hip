@@ -224,7 +224,9 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     a.q_out = w.q;
     a.kc = (char*)w.kc + (size_t)l * page_elems * es;
     a.vc = (char*)w.vc + (size_t)l * page_elems * es;
-    a.page_table = w.pt; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past; a.max_blocks = max_blocks;
+    // pages are allocated contiguously per sequence (identity table written by vcap_decode_init):
+    // the scatter computes page ids instead of loading them (nullptr table)
+    a.page_table = nullptr; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past; a.max_blocks = max_blocks;
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
     // 2) causal attention over the paged cache
     // pages are allocated contiguously per sequence (vcap_decode_init: identity table), so the bf16

@@ -42,9 +42,57 @@ __global__ __launch_bounds__(256) void vcap_patchify_kernel(const float* __restr
   }
 }
 
+// Vectorised im2col for patch sizes that are multiples of 8 (ViT-B/16): one thread per 8
+// consecutive K elements of a patch row (= 8 consecutive pixels of one image row), two 16-byte
+// loads and one 16-byte (bf16) / two (f32) stores; K padding is zero-filled.
+template <typename T>
+__global__ __launch_bounds__(256) void vcap_patchify8_kernel(const float* __restrict__ frames, T* __restrict__ patches,
+                                                             int BT, int img, int p, int Kp) {
+  const int g = img / p, P = g * g, K = 3 * p * p, cpr = Kp / 8;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)BT * P * cpr) return;
+  const long row = i / cpr;
+  const int k = (int)(i % cpr) * 8;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = a;
+  if (k < K) {
+    const int bt = (int)(row / P), pp = (int)(row % P);
+    const int py = pp / g, px = pp % g;
+    const int c = k / (p * p), rem = k % (p * p), y = rem / p, x0 = rem % p;
+    const float* src = frames + (((long)bt * 3 + c) * img + (py * p + y)) * img + px * p + x0;
+    a = *reinterpret_cast<const f32x4*>(src);
+    b = *reinterpret_cast<const f32x4*>(src + 4);
+  }
+  T* dst = patches + row * Kp + k;
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<u32x4*>(dst) = (u32x4){pack_bf2(a.x, a.y), pack_bf2(a.z, a.w), pack_bf2(b.x, b.y),
+                                             pack_bf2(b.z, b.w)};
+  } else {
+    *reinterpret_cast<f32x4*>(dst) = a;
+    *reinterpret_cast<f32x4*>(dst + 4) = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void vcap_cls_rows_kernel(float* __restrict__ x, const float* __restrict__ cls,
+                                                            const float* __restrict__ pos, int N, int D) {
+  float* xr = x + (long)blockIdx.x * N * D;
+  for (int d = threadIdx.x; d < D; d += 256) xr[d] = cls[d] + pos[d];
+}
+
 hipError_t vcap_patchify_dispatch(int dt, const float* frames, void* patches, float* x, const float* cls,
                                   const float* pos, int BT, int img, int p, int Kp, int N, int D, hipStream_t s) {
   const int g = img / p;
+  if (p % 8 == 0 && Kp % 8 == 0 && img % 4 == 0) {
+    const long chunks = (long)BT * g * g * (Kp / 8);
+    const dim3 grid((unsigned)((chunks + 255) / 256));
+    if (dt == VCAP_DT_BF16)
+      hipLaunchKernelGGL((vcap_patchify8_kernel<bf16_t>), grid, dim3(256), 0, s, frames, (bf16_t*)patches, BT, img, p,
+                         Kp);
+    else
+      hipLaunchKernelGGL((vcap_patchify8_kernel<float>), grid, dim3(256), 0, s, frames, (float*)patches, BT, img, p,
+                         Kp);
+    hipLaunchKernelGGL(vcap_cls_rows_kernel, dim3(BT), dim3(256), 0, s, x, cls, pos, N, D);
+    return hipGetLastError();
+  }
   const dim3 grid(BT * g * g + BT), block(256);
   if (dt == VCAP_DT_BF16)
     hipLaunchKernelGGL((vcap_patchify_kernel<bf16_t>), grid, block, 0, s, frames, (bf16_t*)patches, x, cls, pos, BT,

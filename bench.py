@@ -39,8 +39,8 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--batch", type=int, default=8, help="videos per GPU")
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--max-new", type=int, default=24)
@@ -52,10 +52,12 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="no encode/decode overlap (each step's decode finishes before the next encode starts)")
-    ap.add_argument("--reserve-cus", type=int, default=96,
+    ap.add_argument("--reserve-cus", type=int, default=32,
                     help="CUs the encode stream leaves to the decode stream (CU-masked stream; 0 = none)")
     ap.add_argument("--decode-blocks", type=int, default=128,
                     help="cap the decode GEMV grids near this many workgroups (0 = whole-chip grids)")
+    ap.add_argument("--dec-lanes", type=int, default=2,
+                    help="decodes in flight at once (each batch still decoded alone, own stream + graph)")
     ap.add_argument("--cpu-baseline-s", type=float, default=20.0, help="CPU oracle time budget (0 disables)")
     return ap.parse_args()
 
@@ -142,7 +144,8 @@ def main():
     cfg.max_blocks = 0 if args.serial else args.decode_blocks
     gather = (lambda ids: gather_ids(ids, world)) if world > 1 else None
     pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev, gather=gather,
-                           reserve_cus=0 if args.serial else args.reserve_cus)
+                           reserve_cus=0 if args.serial else args.reserve_cus,
+                           dec_lanes=1 if args.serial else args.dec_lanes)
 
     def step(t0=None, t1=None, t2=None):
         pipe.submit(video, t0, t1, t2)
@@ -216,6 +219,9 @@ def main():
                        "decode_block_cap": cfg.max_blocks,
                        "schedule": "serial" if args.serial else
                        f"encode(k+1) overlapped with decode(k) on 2 HIP streams (encode CU-masked off "
+                       f"{args.reserve_cus} CUs)" if args.dec_lanes == 1 else
+                       f"encode(k+{args.dec_lanes}) overlapped with {args.dec_lanes} decodes in flight "
+                       f"(batches k..k+{args.dec_lanes - 1}, one HIP stream + graph each; encode CU-masked off "
                        f"{args.reserve_cus} CUs)"},
             "p50_latency_ms": p50,
             "stage_ms_p50": {"vit_encode_prefix": statistics.median(vit_ms),

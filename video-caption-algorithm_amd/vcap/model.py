@@ -274,8 +274,12 @@ class HipGPT2Decoder:
         return int(N.lib().vcap_gpt2_workspace_bytes(C.byref(self.desc), B, self.prefix_len + prompt_len, max_new))
 
     def generate_ids(self, prefix: torch.Tensor, prompt_ids: Sequence[int], cfg: GenConfig,
-                     out: Optional[torch.Tensor] = None, logits_out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """prefix [B,P,E] f32 device, prompt ids (BOS-only prompt = [eos]) -> int32 [B, max_new] EOS-padded."""
+                     out: Optional[torch.Tensor] = None, logits_out: Optional[torch.Tensor] = None,
+                     workspace: Optional["_Workspace"] = None) -> torch.Tensor:
+        """prefix [B,P,E] f32 device, prompt ids (BOS-only prompt = [eos]) -> int32 [B, max_new] EOS-padded.
+
+        `workspace` (KV pages + decode scratch) defaults to the decoder's own; concurrent decodes on
+        different streams pass one each (the captured graph is keyed on it)."""
         B, P, E = prefix.shape
         if P != self.prefix_len or E != self.arch.n_embd:
             raise ValueError(f"prefix shape {tuple(prefix.shape)} != [B,{self.prefix_len},{self.arch.n_embd}]")
@@ -292,7 +296,7 @@ class HipGPT2Decoder:
                          pad_token_id=int(cfg.pad_token_id), use_graph=int(bool(cfg.use_graph)),
                          max_blocks=int(cfg.max_blocks))
         arr = (C.c_int * max(len(ids), 1))(*ids)
-        ws = self.ws.get(self.workspace_bytes(B, len(ids), mx))
+        ws = (workspace or self.ws).get(self.workspace_bytes(B, len(ids), mx))
         N.check(N.lib().vcap_gpt2_generate(C.byref(self.desc), C.byref(gp), prefix.data_ptr(), arr, len(ids), B,
                                            out.data_ptr(), N.ptr(logits_out), ws.data_ptr(), ws.numel(),
                                            _stream(prefix.device)), "vcap_gpt2_generate")

@@ -6,6 +6,11 @@ streams lets the decode graph's workgroups interleave with the encode GEMMs, so 
 time per batch approaches max(encode, decode) instead of their sum.  Every batch still gets its
 full encode + prefix + decode; double-buffered prefix/ids buffers and events keep batch k+2's
 encode from overwriting buffers batch k's decode still reads.
+
+`dec_lanes` > 1 keeps that many decodes in flight at once (batch k on lane k % dec_lanes, each
+lane its own stream, KV/scratch workspace and captured graph).  A decode is a chain of ~60
+dependent launches per token that occupies a fraction of the CUs it is given, so a second
+independent chain fills the gaps of the first; each batch is still decoded on its own (B rows).
 """
 from __future__ import annotations
 
@@ -16,16 +21,20 @@ import ctypes as C
 import torch
 
 from . import _native as N
-from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder
+from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, _Workspace
 
 
 class CaptionPipeline:
     def __init__(self, encoder: HipViTEncoder, prefix: HipPrefix, decoder: HipGPT2Decoder, cfg: GenConfig,
                  batch: int, prompt_ids: Sequence[int], device, depth: int = 2, gather=None,
-                 reserve_cus: int = 0):
+                 reserve_cus: int = 0, dec_lanes: int = 1):
         self.enc, self.pre, self.dec, self.cfg = encoder, prefix, decoder, cfg
         self.prompt_ids = list(prompt_ids)
         self.device = torch.device(device)
+        if dec_lanes < 1:
+            raise ValueError("dec_lanes must be >= 1")
+        self.lanes = int(dec_lanes)
+        depth = max(int(depth), self.lanes + 1)   # one slot being encoded + one per decoding lane
         self.depth = depth
         # The decode chain is latency-bound: give its stream the higher priority so its small
         # workgroups are dispatched as soon as encode GEMM workgroups retire, and optionally keep
@@ -40,7 +49,9 @@ class CaptionPipeline:
                 self.s_enc = torch.cuda.ExternalStream(self._masked, device=self.device)
             else:
                 self.s_enc = torch.cuda.Stream(self.device, priority=lo)
-            self.s_dec = torch.cuda.Stream(self.device, priority=hi)
+            self.s_decs = [torch.cuda.Stream(self.device, priority=hi) for _ in range(self.lanes)]
+        self.s_dec = self.s_decs[0]
+        self.dec_ws = [decoder.ws] + [_Workspace(self.device) for _ in range(self.lanes - 1)]
         E = decoder.arch.n_embd
         self.prefix_bufs = [torch.empty(batch, prefix.prefix_len, E, device=self.device) for _ in range(depth)]
         self.ids_bufs = [torch.empty(batch, cfg.max_new_tokens, dtype=torch.int32, device=self.device)
@@ -63,9 +74,12 @@ class CaptionPipeline:
             if t_mid is not None:
                 t_mid.record()
             self.enc_done[slot].record()
-        with torch.cuda.stream(self.s_dec):
-            self.s_dec.wait_event(self.enc_done[slot])
-            self.dec.generate_ids(self.prefix_bufs[slot], self.prompt_ids, self.cfg, out=self.ids_bufs[slot])
+        lane = self.k % self.lanes
+        s_dec = self.s_decs[lane]
+        with torch.cuda.stream(s_dec):
+            s_dec.wait_event(self.enc_done[slot])
+            self.dec.generate_ids(self.prefix_bufs[slot], self.prompt_ids, self.cfg, out=self.ids_bufs[slot],
+                                  workspace=self.dec_ws[lane])
             out = self.ids_bufs[slot]
             if self.gather is not None:
                 out = self.gather(out)
@@ -84,7 +98,8 @@ class CaptionPipeline:
 
     def synchronize(self) -> None:
         self.s_enc.synchronize()
-        self.s_dec.synchronize()
+        for s in self.s_decs:
+            s.synchronize()
 
     def close(self) -> None:
         """Drain both streams and release the CU-masked encode stream (if one was created)."""

@@ -138,3 +138,23 @@ def test_bf16_logits_teacher_forced(device):
     first = ids[:, 0].cpu().numpy()
     sure = gap > 0.1
     assert np.array_equal(first[sure], g["hf_greedy_ids"][sure, 0])
+
+
+@pytest.mark.parametrize("lanes,reserve", [(1, 96), (2, 32)])
+def test_pipeline_lanes_fp32_token_identical(device, lanes, reserve):
+    """The bench schedule (vcap/pipeline.py): encode of batch k+lanes on a CU-masked stream while
+    `lanes` decodes run on their own streams / workspaces / graphs; every batch's captions equal
+    the reference's."""
+    from vcap.pipeline import CaptionPipeline
+    meta, g, va, ga, enc, pre, dec, video = _models("b16_b8", "fp32", device)
+    cfg = _hf_cfg(ga)
+    cfg.max_blocks = 128
+    pipe = CaptionPipeline(enc, pre, dec, cfg, video.shape[0], [ga.bos_token_id], device, reserve_cus=reserve,
+                           dec_lanes=lanes)
+    try:
+        slots = [pipe.submit(video) for _ in range(2 * lanes + 1)]
+        for slot in slots[-(lanes + 1):]:
+            got = trim_generated(pipe.result(slot), ga.eos_token_id)
+            assert np.array_equal(np.array(got, dtype=np.int32), g["hf_greedy_ids"])
+    finally:
+        pipe.close()

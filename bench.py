@@ -211,8 +211,8 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": {"bf16": "bf16", "fp8": "mxfp8-e4m3 (ViT QKV/proj/fc1/fc2) + bf16"}.get(args.precision, "f32"),
             "data": "synthetic (seeded U[0,1) frames, ImageNet-normalised; seeded random-init weights)",
             "config": {"workload": f"batch={B} synthetic {T}x3x224x224 videos per GPU, {args.vit} + {args.gpt2}, "
-                                   f"{args.decode} decode max_new {args.max_new} (BASELINE configs[1]"
-                                   f"{'/[2]' if world > 1 else ''})",
+                                   f"{args.decode} decode max_new {args.max_new} (BASELINE "
+                                   f"{'configs[4]-shaped, MXFP8 ViT GEMMs' if args.precision == 'fp8' else 'configs[1]' + ('/[2]' if world > 1 else '')})",
                        "vit": args.vit, "gpt2": args.gpt2, "batch_per_gpu": B, "global_batch": world * B,
                        "frames": T, "max_new_tokens": args.max_new, "decode": args.decode,
                        "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}",

@@ -58,6 +58,9 @@ def parse():
                     help="cap the decode GEMV grids near this many workgroups (0 = whole-chip grids)")
     ap.add_argument("--dec-lanes", type=int, default=2,
                     help="decodes in flight at once (each batch still decoded alone, own stream + graph)")
+    ap.add_argument("--host-e2e", type=int, default=10,
+                    help="iterations of the SURVEY 8(d) latency variant: pinned host frames -> ids on host, "
+                         "one batch at a time (0 disables)")
     ap.add_argument("--cpu-baseline-s", type=float, default=20.0, help="CPU oracle time budget (0 disables)")
     return ap.parse_args()
 
@@ -177,6 +180,22 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
+    # SURVEY 8(d) latency: a host-pinned [B,T,3,H,W] fp32 tensor -> H2D -> encode -> decode ->
+    # token ids on the host, one batch at a time (outside the timed throughput region)
+    host_lat = []
+    if args.host_e2e > 0:
+        pinned = torch.from_numpy(frames_np).pin_memory()
+        vid_h = torch.empty_like(video)
+        for _ in range(args.host_e2e + 1):
+            torch.cuda.synchronize(dev)
+            t_h = time.perf_counter()
+            with torch.cuda.stream(pipe.s_enc):
+                vid_h.copy_(pinned, non_blocking=True)
+            ids_host = pipe.result(pipe.submit(vid_h)).cpu()
+            host_lat.append(time.perf_counter() - t_h)
+        host_lat = host_lat[1:]
+        del ids_host
+
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -250,6 +269,12 @@ def main():
             "vit_flops_per_step": B * T * va.flops_per_frame(),
             "vit_flops_per_step_executed": B * T * va.flops_per_frame(cls_tail=True),
         }
+        if host_lat:
+            hp50 = statistics.median(host_lat)
+            out["host_e2e"] = {"p50_ms": hp50 * 1e3, "captions_per_s": world * B / hp50, "iters": len(host_lat),
+                               "h2d_bytes": int(video.numel() * video.element_size()),
+                               "what": "pinned host fp32 frames -> H2D -> encode -> decode -> ids on host, "
+                                       "one batch at a time (no overlap; rank 0's clock)"}
         if world == 1 and args.cpu_baseline_s > 0:
             out["cpu_baseline"] = cpu_baseline(sd, va, ga, frames_np, args.cpu_baseline_s, args.max_new)
             out["cpu_baseline"].pop("tokens_first", None)

@@ -58,6 +58,8 @@ def parse():
                     help="cap the decode GEMV grids near this many workgroups (0 = whole-chip grids)")
     ap.add_argument("--dec-lanes", type=int, default=2,
                     help="decodes in flight at once (each batch still decoded alone, own stream + graph)")
+    ap.add_argument("--confine-decode", action="store_true",
+                    help="mask the decode streams to the reserved CUs (default: unmasked, high priority)")
     ap.add_argument("--host-e2e", type=int, default=10,
                     help="iterations of the SURVEY 8(d) latency variant: pinned host frames -> ids on host, "
                          "one batch at a time (0 disables)")
@@ -148,7 +150,8 @@ def main():
     gather = (lambda ids: gather_ids(ids, world)) if world > 1 else None
     pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev, gather=gather,
                            reserve_cus=0 if args.serial else args.reserve_cus,
-                           dec_lanes=1 if args.serial else args.dec_lanes)
+                           dec_lanes=1 if args.serial else args.dec_lanes,
+                           confine_decode=args.confine_decode and not args.serial)
 
     def step(t0=None, t1=None, t2=None):
         pipe.submit(video, t0, t1, t2)
@@ -189,12 +192,15 @@ def main():
         for _ in range(args.host_e2e + 1):
             torch.cuda.synchronize(dev)
             t_h = time.perf_counter()
-            with torch.cuda.stream(pipe.s_enc):
-                vid_h.copy_(pinned, non_blocking=True)
+            # H2D on torch's own stream (the pinned-memory allocator records its event there, not on
+            # the pipeline's external CU-masked stream that close() destroys); the encode waits on it
+            vid_h.copy_(pinned, non_blocking=True)
+            pipe.s_enc.wait_stream(torch.cuda.current_stream(dev))
             ids_host = pipe.result(pipe.submit(vid_h)).cpu()
             host_lat.append(time.perf_counter() - t_h)
         host_lat = host_lat[1:]
-        del ids_host
+        torch.cuda.synchronize(dev)
+        del ids_host, pinned, vid_h
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:

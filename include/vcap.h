@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 4
+#define VCAP_ABI_VERSION 5
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -211,6 +211,14 @@ int vcap_gpt2_step(const vcap_gpt2_desc* d, const int* tokens, int rows, int S0,
                    float* logits_out, void* workspace, size_t ws_bytes, void* stream);
 int vcap_gpt2_reorder(const vcap_gpt2_desc* d, const int* src_rows, int rows, int S0, int max_new_tokens, int length,
                       void* workspace, size_t ws_bytes, void* stream);
+/* ---- the same state driven by input EMBEDDINGS (HF `GPT2LMHeadModel(inputs_embeds=...,
+ *      past_key_values=..., use_cache=True)` as core/scripts/benchmark_baseline.py:160-240 calls
+ *      it through `model.decoder.model`): past_len == 0 -> prefill of n_tok == S0 positions
+ *      (rows sequences, embeds [rows, S0, E] f32); past_len > 0 -> one position (n_tok == 1,
+ *      embeds [rows, 1, E]) at S0 <= past_len < S0 + max_new_tokens.  h = embeds + wpe[pos];
+ *      logits of each row's last position -> [rows, vocab] f32.  Same workspace as above. ---- */
+int vcap_gpt2_forward_embeds(const vcap_gpt2_desc* d, const float* embeds, int rows, int n_tok, int past_len, int S0,
+                             int max_new_tokens, float* logits_out, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- live kernel timing for the benchmark's roofline (sites: "vit.qkv", "vit.attention",
  *      "vit.proj", "vit.fc1", "vit.fc2"): events are recorded around each launch of the site on

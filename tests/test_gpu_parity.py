@@ -158,3 +158,40 @@ def test_pipeline_lanes_fp32_token_identical(device, lanes, reserve):
             assert np.array_equal(np.array(got, dtype=np.int32), g["hf_greedy_ids"])
     finally:
         pipe.close()
+
+
+@pytest.mark.parametrize("name", ["tiny", "tiny_prompt", "b16_b8"])
+def test_decoder_model_forward_raw_greedy(device, name):
+    """`model.decoder.model(inputs_embeds=..., past_key_values=..., use_cache=True)` driven by the
+    reference benchmark's own loop (core/scripts/benchmark_baseline.py:160-240, restated here):
+    token-identical to the reference's raw-greedy ids, first-step logits within 1e-3."""
+    from vcap.caption import HipVideoCaptionModel
+    from helpers import case as _case
+    meta, g, va, ga, sd, frames = _case(name)
+    m = HipVideoCaptionModel(sd, meta["vit"], meta["gpt2"], 4, "fp32", device)
+    _, prefix = m.encode_prefix(torch.from_numpy(frames).to(device), 0.6, 0.4)
+    gpt2, eos = m.decoder.model, ga.eos_token_id
+    B = prefix.shape[0]
+    prompt = list(meta["prompt_ids"]) or [ga.bos_token_id]
+    pids = torch.tensor([prompt], dtype=torch.long, device=device).expand(B, -1)
+    nxt = torch.cat([prefix, gpt2.transformer.wte(pids)], dim=1)
+    mask = torch.ones(nxt.shape[:2], dtype=torch.long, device=device)
+    past, toks = None, [[] for _ in range(B)]
+    finished = torch.zeros(B, dtype=torch.bool, device=device)
+    for step in range(24):
+        out = gpt2(inputs_embeds=nxt, attention_mask=mask, past_key_values=past, use_cache=True, return_dict=True)
+        logits = out.logits[:, -1, :]
+        if step == 0 and "hf_greedy_logits" in g:
+            np.testing.assert_allclose(logits.cpu().numpy(), g["hf_greedy_logits"][:, 0], atol=1e-3, rtol=0)
+        t = torch.argmax(logits, dim=-1)
+        t = torch.where(finished, torch.full_like(t, eos), t)
+        for i, v in enumerate(t.tolist()):
+            if not finished[i]:
+                toks[i].append(v)
+                finished[i] = v == eos
+        past = out.past_key_values
+        if bool(finished.all()):
+            break
+        nxt = gpt2.transformer.wte(t).unsqueeze(1)
+        mask = torch.cat([mask, torch.ones((B, 1), dtype=torch.long, device=device)], dim=1)
+    assert np.array_equal(pad_rows(toks, 24), g["raw_greedy_ids"]), (toks, g["raw_greedy_ids"])

@@ -579,12 +579,12 @@ template <typename T>
 __global__ __launch_bounds__(256) void vcap_prefill_embed_kernel(const float* __restrict__ prefix, int P,
                                                                  PromptIds prompt, const T* __restrict__ wte,
                                                                  const float* __restrict__ wpe, float* __restrict__ h,
-                                                                 int S0, int E) {
+                                                                 int S0, int E, int pos0) {
   const int m = blockIdx.x;
   const int s = m / S0, i = m % S0;
   for (int c = threadIdx.x; c < E; c += 256) {
     float v = (i < P) ? prefix[((long)s * P + i) * E + c] : Num<T>::to_f(wte[(long)prompt.ids[i - P] * E + c]);
-    h[(long)m * E + c] = v + wpe[(long)i * E + c];
+    h[(long)m * E + c] = v + wpe[(long)(pos0 + i) * E + c];
   }
 }
 
@@ -911,7 +911,7 @@ hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc,
 }
 
 hipError_t vcap_prefill_embed_dispatch(int dt, const float* prefix, int P, const int* ids, int nids, const void* wte,
-                                       const float* wpe, float* h, int B, int E, hipStream_t s) {
+                                       const float* wpe, float* h, int B, int E, hipStream_t s, int pos0) {
   if (nids > 64) return hipErrorInvalidValue;
   PromptIds pr;
   pr.n = nids;
@@ -919,10 +919,10 @@ hipError_t vcap_prefill_embed_dispatch(int dt, const float* prefix, int P, const
   const int S0 = P + nids;
   if (dt == VCAP_DT_BF16)
     hipLaunchKernelGGL((vcap_prefill_embed_kernel<bf16_t>), dim3(B * S0), dim3(256), 0, s, prefix, P, pr,
-                       (const bf16_t*)wte, wpe, h, S0, E);
+                       (const bf16_t*)wte, wpe, h, S0, E, pos0);
   else
     hipLaunchKernelGGL((vcap_prefill_embed_kernel<float>), dim3(B * S0), dim3(256), 0, s, prefix, P, pr,
-                       (const float*)wte, wpe, h, S0, E);
+                       (const float*)wte, wpe, h, S0, E, pos0);
   return hipGetLastError();
 }
 

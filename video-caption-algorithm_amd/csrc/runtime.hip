@@ -784,6 +784,29 @@ int vcap_gpt2_step(const vcap_gpt2_desc* d, const int* tokens, int rows, int S0,
   return run_lm_head(d, w, rows, 1, logits_out, 1, 0, 1.0f, 0, -1, &nblk, s);
 }
 
+int vcap_gpt2_forward_embeds(const vcap_gpt2_desc* d, const float* embeds, int rows, int n_tok, int past_len, int S0,
+                             int max_new_tokens, float* logits_out, void* workspace, size_t ws_bytes, void* stream) {
+  if (!embeds || !logits_out || rows <= 0) return fail(VCAP_E_ARG, "vcap_gpt2_forward_embeds: bad arguments");
+  if (past_len == 0 ? n_tok != S0 : (n_tok != 1 || past_len < S0 || past_len >= S0 + max_new_tokens))
+    return fail(VCAP_E_ARG, "vcap_gpt2_forward_embeds: prefill needs n_tok == S0; a step one token at "
+                            "S0 <= past_len < S0 + max_new_tokens");
+  if (past_len == 0 && rows * S0 > 128) return fail(VCAP_E_UNSUPPORTED, "rows*S0 must be <= 128 at prefill");
+  DecBufs w;
+  int maxp;
+  size_t pe;
+  void* scratch;
+  if (int rc = step_setup(d, rows, S0, max_new_tokens, workspace, ws_bytes, &w, &maxp, &pe, &scratch)) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (past_len == 0) VCAP_TRY(vcap_decode_init_dispatch(w.pt, rows, maxp, w.finished, w.nbanned, s), "decode_init");
+  // the prefill-embedding kernel with every position taken from `embeds` (P = n_tok, no prompt ids)
+  VCAP_TRY(vcap_prefill_embed_dispatch(d->dtype, embeds, n_tok, nullptr, 0, d->wte, d->wpe, w.h, rows, d->n_embd, s,
+                                       past_len),
+           "embed_inputs");
+  if (int rc = run_layers(d, w, maxp, pe, rows * n_tok, n_tok, past_len, 0, s)) return rc;
+  int nblk;
+  return run_lm_head(d, w, rows, n_tok, logits_out, 1, 0, 1.0f, 0, -1, &nblk, s);
+}
+
 int vcap_gpt2_reorder(const vcap_gpt2_desc* d, const int* src_rows, int rows, int S0, int max_new_tokens, int length,
                       void* workspace, size_t ws_bytes, void* stream) {
   if (!src_rows || length <= 0) return fail(VCAP_E_ARG, "vcap_gpt2_reorder: bad arguments");

@@ -16,7 +16,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
 DT_F32, DT_BF16, DT_MXFP8 = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
@@ -95,6 +95,7 @@ SIGNATURES = {
     "vcap_gpt2_prefill": (i32, [C.POINTER(GPT2Desc), vp, C.POINTER(C.c_int), i32, i32, i32, i32, vp, vp, sz, vp]),
     "vcap_gpt2_step": (i32, [C.POINTER(GPT2Desc), vp, i32, i32, i32, i32, vp, vp, sz, vp]),
     "vcap_gpt2_reorder": (i32, [C.POINTER(GPT2Desc), vp, i32, i32, i32, i32, vp, sz, vp]),
+    "vcap_gpt2_forward_embeds": (i32, [C.POINTER(GPT2Desc), vp, i32, i32, i32, i32, i32, vp, vp, sz, vp]),
     "vcap_probe_enable": (i32, [C.c_char_p, i32]),
     "vcap_probe_read": (i32, [C.c_char_p, fp, C.POINTER(C.c_int)]),
 }

@@ -6,6 +6,8 @@ Surface kept from the reference (src/models/caption_model.py:11-101, text_decode
   model.decoder.mapper(emb)       -> [B, P*E] f32       (Linear 256 -> P*E; Dropout is eval-identity)
   model.decoder.generate(emb, prompt, **kw) -> list[str]   (HF generate semantics, see below)
   model.decoder.tokenizer / .cond_mode / .prefix_len / .model.config.n_embd / .model.transformer.wte
+  model.decoder.model(inputs_embeds=, attention_mask=, past_key_values=, use_cache=True)
+                                  (GPT2LMHeadModel forward as benchmark_baseline.py:160-240 calls it)
   model.generate(video, prompt, **kw)       (VideoCaptionModel.generate: no engine LN-scale)
 plus the batched fast path `generate_ids(video, prompt_ids, ...)` -> int32 [B, max_new] on device.
 
@@ -15,12 +17,14 @@ num_beams > 1 -> beam search; num_beams == 1 and temperature != 1 -> sampling (t
 """
 from __future__ import annotations
 
+import ctypes as C
 from types import SimpleNamespace
 from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
 
+from . import _native as N
 from . import configs
 from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, trim_generated
 from .tokenizer import load_tokenizer
@@ -51,6 +55,69 @@ class _WTE:
         return self.weight[ids.to(self.weight.device)].float()
 
 
+class HipPast:
+    """`past_key_values` of the HIP decoder: the paged KV state lives in a workspace carved for
+    `rows` sequences of S0 prefill positions + up to `capacity` appended ones."""
+
+    def __init__(self, hip: HipGPT2Decoder, rows: int, S0: int, capacity: int):
+        self.hip, self.rows, self.S0, self.capacity = hip, rows, S0, capacity
+        nbytes = int(N.lib().vcap_gpt2_beam_workspace_bytes(C.byref(hip.desc), rows, S0, capacity))
+        self.ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=hip.device)
+        self.length = 0
+
+    def get_seq_length(self) -> int:
+        return self.length
+
+
+class HipGPT2LMHead:
+    """`decoder.model`: GPT2LMHeadModel's forward as core/scripts/benchmark_baseline.py:160-240
+    drives it - `model(inputs_embeds=, attention_mask=, past_key_values=, use_cache=True,
+    return_dict=True)` -> `.logits`, `.past_key_values` - on vcap_gpt2_forward_embeds.
+
+    The first call (past_key_values None) prefills the whole `inputs_embeds` [B, L, E]; later
+    calls append one position per row.  `.logits` holds the LAST position only ([B, 1, vocab]),
+    which is what every caller reads (`outputs.logits[:, -1, :]`).  attention_mask must be all
+    ones (no padding on this path)."""
+
+    def __init__(self, hip: HipGPT2Decoder, arch: configs.GPT2Arch, wte: "_WTE", max_cache_tokens: int = 128):
+        self.hip, self.arch = hip, arch
+        self.config = SimpleNamespace(n_embd=arch.n_embd, n_layer=arch.n_layer, n_head=arch.n_head,
+                                      vocab_size=arch.vocab)
+        self.transformer = SimpleNamespace(wte=wte)
+        self.max_cache_tokens = max_cache_tokens
+
+    def __call__(self, input_ids=None, inputs_embeds=None, attention_mask=None, past_key_values=None,
+                 use_cache: bool = True, return_dict: bool = True):
+        if inputs_embeds is None:
+            if input_ids is None:
+                raise ValueError("give input_ids or inputs_embeds")
+            inputs_embeds = self.transformer.wte(input_ids)
+        x = inputs_embeds.to(self.hip.device, torch.float32).contiguous()
+        B, L, E = x.shape
+        if E != self.arch.n_embd:
+            raise ValueError(f"inputs_embeds last dim {E} != n_embd {self.arch.n_embd}")
+        if attention_mask is not None and not bool((attention_mask != 0).all()):
+            raise NotImplementedError("padded attention masks are not supported on the HIP decode path")
+        past = past_key_values
+        if past is None:
+            cap = min(self.max_cache_tokens, self.arch.n_positions - L)
+            past = HipPast(self.hip, B, L, cap)
+        elif not isinstance(past, HipPast):
+            raise TypeError("past_key_values must come from a previous call of this model")
+        elif L != 1 or B != past.rows:
+            raise ValueError("after the prefill, feed one position per row ([rows, 1, E])")
+        elif past.length >= past.S0 + past.capacity:
+            raise ValueError(f"KV capacity exhausted ({past.capacity} appended positions; raise max_cache_tokens)")
+        logits = torch.empty(B, self.arch.vocab, dtype=torch.float32, device=self.hip.device)
+        N.check(N.lib().vcap_gpt2_forward_embeds(C.byref(self.hip.desc), x.data_ptr(), B, L, past.length, past.S0,
+                                                 past.capacity, logits.data_ptr(), past.ws.data_ptr(),
+                                                 past.ws.numel(), torch.cuda.current_stream(self.hip.device).cuda_stream),
+                "vcap_gpt2_forward_embeds")
+        past.length += L
+        out = SimpleNamespace(logits=logits[:, None, :], past_key_values=past if use_cache else None)
+        return out if return_dict else (out.logits, out.past_key_values)
+
+
 class HipTextDecoder:
     def __init__(self, sd, arch: configs.GPT2Arch, precision: str, device, prefix_len: int = 4,
                  tokenizer_dir: str = "", use_graph: bool = True):
@@ -59,9 +126,7 @@ class HipTextDecoder:
         self.mapper_op = HipPrefix(sd, arch.n_embd, prefix_len, 0.0, 0.0, device)
         self.tokenizer = load_tokenizer(tokenizer_dir, arch.eos_token_id)
         self.use_graph = use_graph
-        self.model = SimpleNamespace(config=SimpleNamespace(n_embd=arch.n_embd, n_layer=arch.n_layer,
-                                                            n_head=arch.n_head, vocab_size=arch.vocab),
-                                     transformer=SimpleNamespace(wte=_WTE(self.hip.wte)))
+        self.model = HipGPT2LMHead(self.hip, arch, _WTE(self.hip.wte))
 
     def mapper(self, emb: torch.Tensor) -> torch.Tensor:
         """Linear 256 -> P*E on the HIP path (cupy_linear_mapper / CuPyLinearCompat replacement)."""

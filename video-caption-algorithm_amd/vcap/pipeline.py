@@ -27,7 +27,7 @@ from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, _Workspa
 class CaptionPipeline:
     def __init__(self, encoder: HipViTEncoder, prefix: HipPrefix, decoder: HipGPT2Decoder, cfg: GenConfig,
                  batch: int, prompt_ids: Sequence[int], device, depth: int = 2, gather=None,
-                 reserve_cus: int = 0, dec_lanes: int = 1):
+                 reserve_cus: int = 0, dec_lanes: int = 1, confine_decode: bool = False):
         self.enc, self.pre, self.dec, self.cfg = encoder, prefix, decoder, cfg
         self.prompt_ids = list(prompt_ids)
         self.device = torch.device(device)
@@ -49,7 +49,21 @@ class CaptionPipeline:
                 self.s_enc = torch.cuda.ExternalStream(self._masked, device=self.device)
             else:
                 self.s_enc = torch.cuda.Stream(self.device, priority=lo)
-            self.s_decs = [torch.cuda.Stream(self.device, priority=hi) for _ in range(self.lanes)]
+            self._dec_handles = []
+            if confine_decode and reserve_cus > 0:
+                # decode streams masked to exactly the reserved CUs: decode workgroups never take
+                # an encode CU between two GEMM workgroups
+                words = (torch.cuda.get_device_properties(self.device).multi_processor_count + 31) // 32
+                mask = (C.c_uint32 * words)()
+                for c in range(reserve_cus):
+                    mask[c // 32] |= 1 << (c % 32)
+                for _ in range(self.lanes):
+                    h = C.c_void_p()
+                    N.check(N.lib().vcap_stream_create_cu_mask(mask, words, C.byref(h)), "decode stream")
+                    self._dec_handles.append(h.value)
+                self.s_decs = [torch.cuda.ExternalStream(h, device=self.device) for h in self._dec_handles]
+            else:
+                self.s_decs = [torch.cuda.Stream(self.device, priority=hi) for _ in range(self.lanes)]
         self.s_dec = self.s_decs[0]
         self.dec_ws = [decoder.ws] + [_Workspace(self.device) for _ in range(self.lanes - 1)]
         E = decoder.arch.n_embd
@@ -107,3 +121,6 @@ class CaptionPipeline:
         if self._masked is not None:
             N.check(N.lib().vcap_stream_destroy(self._masked), "stream destroy")
             self._masked = None
+        for h in self._dec_handles:
+            N.check(N.lib().vcap_stream_destroy(h), "stream destroy")
+        self._dec_handles = []

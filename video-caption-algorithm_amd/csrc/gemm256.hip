@@ -336,15 +336,55 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
           amax = rows_max(amax);
           const int sbyte = mx_scale_byte(amax);
           const float inv = mx_inv_scale(sbyte);
+          // lanes fg, fg ^ 1 trade halves so each stores 8 contiguous bytes (one dwordx2 instead
+          // of two dword stores): even lane columns [8k, 8k+8) of j = 0, odd [16+8k, +8) of j = 1
+          const bool odd = (lane & 16) != 0;
+          const f32x4 q0 = v[0] * inv, q1 = v[1] * inv;
+          const uint32_t p0 = pack_fp8x4(q0.x, q0.y, q0.z, q0.w), p1 = pack_fp8x4(q1.x, q1.y, q1.z, q1.w);
+          const uint32_t r = (uint32_t)xor16_i((int)(odd ? p0 : p1));
           if (m < M && nb < N) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const f32x4 q = v[j] * inv;
-              *reinterpret_cast<uint32_t*>((uint8_t*)C + (long)m * ldc + nb + j * 16 + fg * 4) =
-                  pack_fp8x4(q.x, q.y, q.z, q.w);
-            }
+            *reinterpret_cast<u32x2*>((uint8_t*)C + (long)m * ldc + nb + (odd ? 12 + 4 * fg : 4 * fg)) =
+                odd ? (u32x2){r, p1} : (u32x2){p0, r};
             if (fg == 0) epi.c_scale[mx_scale_index(m, nb, (M + 255) >> 8)] = (uint8_t)sbyte;
           }
+        }
+      }
+  } else if (sizeof(TOut) == 2 && (EPI == 0 || EPI == 1) && (N & 31) == 0 && (ldc & 7) == 0 &&
+             ((uintptr_t)C & 15) == 0) {
+    // bf16 out, 16-byte stores: lanes fg and fg ^ 1 (lane ^ 16) trade halves so the even lane
+    // holds columns [8k, 8k+8) of the j = 0 tile and the odd lane [16+8k, +8) of the j = 1 tile
+    // (k = fg >> 1); one dwordx4 store per row instead of two dwordx2 (the epilogue's store
+    // issue, not HBM bandwidth, is what the row-per-lane dwordx2 pattern pays for)
+    const bool odd = (lane & 16) != 0;
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn) {
+        const int nb = n0 + wc * 64 + qn * 32;
+        f32x4 bias[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bias[j] = epi.bias ? *reinterpret_cast<const f32x4*>(epi.bias + min(nb + j * 16 + fg * 4, N - 4))
+                             : (f32x4){0.f, 0.f, 0.f, 0.f};
+        const int col = nb + (odd ? 12 + 4 * fg : 4 * fg);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wr * 128 + qm * 64 + i * 16 + fr;
+          uint32_t p[2][2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            f32x4 v = acc[qm][qn][i][j] + bias[j];
+            if constexpr (EPI == 1) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+            }
+            p[j][0] = pack_bf2(v.x, v.y);
+            p[j][1] = pack_bf2(v.z, v.w);
+          }
+          const uint32_t r0 = (uint32_t)xor16_i((int)(odd ? p[0][0] : p[1][0]));
+          const uint32_t r1 = (uint32_t)xor16_i((int)(odd ? p[0][1] : p[1][1]));
+          const u32x4 o = odd ? (u32x4){r0, r1, p[1][0], p[1][1]} : (u32x4){p[0][0], p[0][1], r0, r1};
+          if (m < M && nb < N) *reinterpret_cast<u32x4*>(C + (long)m * ldc + col) = o;
         }
       }
   } else {

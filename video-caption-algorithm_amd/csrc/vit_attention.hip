@@ -307,19 +307,33 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
         amax = rows_max(amax);
         const int sb = mx_scale_byte(amax);
         const float is = mx_inv_scale(sb);
+        // lanes fg, fg ^ 1 trade halves: one 8-byte store each (even: bytes [8k, 8k+8) of the
+        // first 16, odd: [16 + 8k, +8))
+        const bool odd = (threadIdx.x & 16) != 0;
+        const uint32_t p0 = pack_fp8x4(v0.x * is, v0.y * is, v0.z * is, v0.w * is);
+        const uint32_t p1 = pack_fp8x4(v1.x * is, v1.y * is, v1.z * is, v1.w * is);
+        const uint32_t r = (uint32_t)xor16_i((int)(odd ? p0 : p1));
         if (keep) {
           uint8_t* orow = (uint8_t*)out + row * D + h * 64 + 32 * b;
-          *reinterpret_cast<uint32_t*>(orow + 4 * fg) = pack_fp8x4(v0.x * is, v0.y * is, v0.z * is, v0.w * is);
-          *reinterpret_cast<uint32_t*>(orow + 16 + 4 * fg) = pack_fp8x4(v1.x * is, v1.y * is, v1.z * is, v1.w * is);
+          *reinterpret_cast<u32x2*>(orow + (odd ? 12 + 4 * fg : 4 * fg)) = odd ? (u32x2){r, p1} : (u32x2){p0, r};
           if (fg == 0) oscale[mx_scale_index((int)row, h * 64 + 32 * b, groups)] = (uint8_t)sb;
         }
       }
-    } else if (keep) {
+    } else {
+      // O[q][d = dt*16 + 4*fg + r]; lanes fg, fg ^ 1 (lane ^ 16) trade halves of the dt pair
+      // (2k, 2k+1) so each stores 8 contiguous dims with one dwordx4 (the even lane dims
+      // [32k + 4fg, +8), the odd lane [32k + 12 + 4fg, +8)); the exchange runs in every lane
+      const bool odd = (threadIdx.x & 16) != 0;
       bf16_t* orow = (bf16_t*)out + row * D + h * 64;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const f32x4 v = o[dt] * inv;  // O[q][d = dt*16 + 4*fg + r]
-        *reinterpret_cast<u32x2*>(orow + dt * 16 + 4 * fg) = (u32x2){cvt_pk_bf16(v.x, v.y), cvt_pk_bf16(v.z, v.w)};
+      for (int k = 0; k < 2; ++k) {
+        const f32x4 va = o[2 * k] * inv, vb = o[2 * k + 1] * inv;
+        const uint32_t a0 = cvt_pk_bf16(va.x, va.y), a1 = cvt_pk_bf16(va.z, va.w);
+        const uint32_t b0 = cvt_pk_bf16(vb.x, vb.y), b1 = cvt_pk_bf16(vb.z, vb.w);
+        const uint32_t r0 = (uint32_t)xor16_i((int)(odd ? a0 : b0));
+        const uint32_t r1 = (uint32_t)xor16_i((int)(odd ? a1 : b1));
+        const u32x4 w = odd ? (u32x4){r0, r1, b0, b1} : (u32x4){a0, a1, r0, r1};
+        if (keep) *reinterpret_cast<u32x4*>(orow + 32 * k + (odd ? 12 + 4 * fg : 4 * fg)) = w;
       }
     }
   }

@@ -60,6 +60,7 @@ def parse():
                     help="decodes in flight at once (each batch still decoded alone, own stream + graph)")
     ap.add_argument("--confine-decode", action="store_true",
                     help="mask the decode streams to the reserved CUs (default: unmasked, high priority)")
+    ap.add_argument("--gemm-policy", type=int, default=0, help="vcap_set_gemm_policy value for A/B runs (0 = auto)")
     ap.add_argument("--host-e2e", type=int, default=10,
                     help="iterations of the SURVEY 8(d) latency variant: pinned host frames -> ids on host, "
                          "one batch at a time (0 disables)")
@@ -139,6 +140,7 @@ def main():
     frames_np = prng.imagenet_frames(1000 + rank, (B, T, 3, va.image, va.image))   # distinct videos per rank
     video = torch.from_numpy(frames_np).to(dev)
 
+    N.check(N.lib().vcap_set_gemm_policy(args.gemm_policy), "gemm policy")
     enc = HipViTEncoder(sd, va, args.precision, dev)
     pre = HipPrefix(sd, ga.n_embd, device=dev)
     dec = HipGPT2Decoder(sd, ga, "bf16" if args.precision == "fp8" else args.precision, dev)

@@ -81,9 +81,13 @@ __global__ __launch_bounds__(256) void vcap_gemm_kernel(const TIn* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / BK;
-  stage_tile(A, lda, m0, M, 0, smem, wave, lane);
-  stage_tile(W, ldw, n0, N, 0, smem + TILE_BYTES, wave, lane);
+  // split-K (gridDim.y > 1): this workgroup sums K-tiles [kt0, kt0 + nk) and adds its partial
+  // into C (f32, residual already in place) with float atomics; split 0 adds the bias
+  const int nk = K / BK / (int)gridDim.y;
+  const int kt0 = (int)blockIdx.y * nk;
+  const bool split = gridDim.y > 1;
+  stage_tile(A, lda, m0, M, kt0 * BK, smem, wave, lane);
+  stage_tile(W, ldw, n0, N, kt0 * BK, smem + TILE_BYTES, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -92,8 +96,8 @@ __global__ __launch_bounds__(256) void vcap_gemm_kernel(const TIn* __restrict__ 
     char* cur = smem + (kt & 1) * STAGE_BYTES;
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-      stage_tile(A, lda, m0, M, (kt + 1) * BK, nxt, wave, lane);
-      stage_tile(W, ldw, n0, N, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+      stage_tile(A, lda, m0, M, (kt0 + kt + 1) * BK, nxt, wave, lane);
+      stage_tile(W, ldw, n0, N, (kt0 + kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
     }
     const char* ta = cur;
     const char* tb = cur + TILE_BYTES;
@@ -104,41 +108,72 @@ __global__ __launch_bounds__(256) void vcap_gemm_kernel(const TIn* __restrict__ 
       for (int i = 0; i < 4; ++i) af[i] = lds_frag(ta, wm * 64 + i * 16 + fr, s * 4 + fg);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = lds_frag(tb, wn * 64 + j * 16 + fr, s * 4 + fg);
+      // weight fragment as the MFMA A operand: a lane ends up with 4 consecutive COLUMNS of
+      // one row, so the epilogue stores vectors
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_frag(af[i], bfr[j], acc[i][j], (TIn*)nullptr);
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_frag(bfr[j], af[i], acc[i][j], (TIn*)nullptr);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   (void)E;
 
-  // epilogue: lane holds rows fg*4 + r, column fr of each 16x16 tile
+  // epilogue: lane holds row fr, columns 4*fg .. 4*fg+3 of each 16x16 tile
+  const bool vec = (N & 3) == 0 && (ldc & 3) == 0 && (!epi.res || (epi.ldr & 3) == 0);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + fr;
-    if (n >= N) continue;
-    const float bias = epi.bias ? epi.bias[n] : 0.f;
+    const int nb = n0 + wn * 64 + j * 16 + 4 * fg;
+    if (nb >= N) continue;
+    float bias[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[e] = (epi.bias && nb + e < N && (!split || blockIdx.y == 0)) ? epi.bias[nb + e] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + fr;
+      if (m >= M) continue;
+      long orow = m;
+      if constexpr (EPI == 3) orow = epi.G ? (long)(m / epi.G) * epi.Gs + epi.goff + (m % epi.G) : (long)m;
+      float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + i * 16 + fg * 4 + r;
-        if (m >= M) continue;
-        float v = acc[i][j][r] + bias;
-        long orow = m;
-        if constexpr (EPI == 1) {
-          v = gelu_tanh(v);
-        } else if constexpr (EPI == 2) {
-          v += epi.res[orow * epi.ldr + n];
-        } else if constexpr (EPI == 3) {
-          if (epi.act == 1) v = gelu_tanh(v);
-          orow = epi.G ? (long)(m / epi.G) * epi.Gs + epi.goff + (m % epi.G) : (long)m;
-          if (epi.res_mode == 1) v += epi.res[orow * epi.ldr + n];
-          else if (epi.res_mode == 2) v += epi.res[(long)((m % epi.G) + epi.roff) * epi.ldr + n];
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bias[e];
+      if (split) {  // f32 C that already holds the residual (dispatcher)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (nb + e < N) atomicAdd((float*)C + orow * ldc + nb + e, v[e]);
+        continue;
+      }
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+      } else if constexpr (EPI == 3) {
+        if (epi.act == 1)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+      }
+      const float* rr = nullptr;
+      if constexpr (EPI == 2) rr = epi.res + orow * epi.ldr + nb;
+      if constexpr (EPI == 3) {
+        if (epi.res_mode == 1) rr = epi.res + orow * epi.ldr + nb;
+        else if (epi.res_mode == 2) rr = epi.res + (long)((m % epi.G) + epi.roff) * epi.ldr + nb;
+      }
+      if (vec && nb + 3 < N) {
+        if (rr) {
+          const f32x4 r = *reinterpret_cast<const f32x4*>(rr);
+          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
         }
-        C[orow * ldc + n] = Num<TOut>::from_f(v);
+        if constexpr (sizeof(TOut) == 2) {
+          *reinterpret_cast<u32x2*>(C + orow * ldc + nb) = (u32x2){pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+        } else {
+          *reinterpret_cast<f32x4*>(C + orow * ldc + nb) = (f32x4){v[0], v[1], v[2], v[3]};
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (nb + e >= N) continue;
+          C[orow * ldc + nb + e] = Num<TOut>::from_f(v[e] + (rr ? rr[e] : 0.f));
+        }
       }
     }
   }
@@ -148,7 +183,24 @@ template <typename TIn, typename TOut, int EPI>
 static hipError_t launch_gemm_epi(const void* A, long lda, const void* W, long ldw, void* C, long ldc, int M, int N,
                                   int K, const GemmEpi& epi, hipStream_t s) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((vcap_gemm_kernel<TIn, TOut, EPI>), dim3(tiles), dim3(256), 0, s, (const TIn*)A, lda,
+  // Few tiles (the CLS-only last block: M = B*T rows) leave most CUs idle through a long K
+  // loop: split K over up to 16 workgroups per tile when C is f32 and already holds the
+  // residual (attn-proj / fc2 in place), adding partials with float atomics (bf16 operands
+  // only: the fp32 parity mode keeps one fixed summation order).
+  int splits = 1;
+  if constexpr (sizeof(TIn) == 2 && sizeof(TOut) == 4) {
+    const bool in_place = epi.bias != nullptr && epi.res == (const float*)C && epi.ldr == ldc &&
+                          (EPI == 2 || (EPI == 3 && epi.res_mode == 1 && epi.act == 0));
+    const int nkt = K / (ROWB / (int)sizeof(TIn));
+    const int ncu = vcap_stream_cus(s);
+    if (in_place && tiles * 4 <= ncu)
+      for (int c = 16; c >= 2; --c)
+        if (nkt % c == 0 && tiles * c <= 2 * ncu) {
+          splits = c;
+          break;
+        }
+  }
+  hipLaunchKernelGGL((vcap_gemm_kernel<TIn, TOut, EPI>), dim3(tiles, splits), dim3(256), 0, s, (const TIn*)A, lda,
                      (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, epi);
   return hipGetLastError();
 }

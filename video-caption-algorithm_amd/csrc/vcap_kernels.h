@@ -54,6 +54,8 @@ struct RowsGemmArgs {
 hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
                               long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s);
 int vcap_gemm_k_align(int in_dt);
+// CUs a launch on stream s may use (its CU mask, else the device's CU count)
+int vcap_stream_cus(hipStream_t s);
 bool vcap_gemm256_ok(int in_dt, int out_dt, long lda, long ldw, long ldc, int M, int N, int K, const GemmEpi& epi);
 hipError_t vcap_gemm256_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
                                  long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s);

@@ -184,7 +184,7 @@ static hipError_t launch_gemm_epi(const void* A, long lda, const void* W, long l
                                   int K, const GemmEpi& epi, hipStream_t s) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   // Few tiles (the CLS-only last block: M = B*T rows) leave most CUs idle through a long K
-  // loop: split K over up to 16 workgroups per tile when C is f32 and already holds the
+  // loop: split K over several workgroups per tile when C is f32 and already holds the
   // residual (attn-proj / fc2 in place), adding partials with float atomics (bf16 operands
   // only: the fp32 parity mode keeps one fixed summation order).
   int splits = 1;
@@ -193,9 +193,11 @@ static hipError_t launch_gemm_epi(const void* A, long lda, const void* W, long l
                           (EPI == 2 || (EPI == 3 && epi.res_mode == 1 && epi.act == 0));
     const int nkt = K / (ROWB / (int)sizeof(TIn));
     const int ncu = vcap_stream_cus(s);
-    if (in_place && tiles * 4 <= ncu)
+    // (the partials' float atomics, not the K loop, dominate past a few splits: keep >= 3 K-tiles
+    // per workgroup and the grid within a quarter of the CUs)
+    if (in_place && tiles * 8 <= ncu)
       for (int c = 16; c >= 2; --c)
-        if (nkt % c == 0 && tiles * c <= 2 * ncu) {
+        if (nkt % c == 0 && nkt / c >= 3 && tiles * c * 4 <= ncu) {
           splits = c;
           break;
         }

@@ -12,7 +12,7 @@ import torch  # noqa: E402
 
 from vcap import _native as N  # noqa: E402
 
-args = sys.argv[1:]
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
 M = int(args.pop(0)) if args and args[0].isdigit() else 25216
 variants = []
 for a in args:
@@ -34,6 +34,8 @@ def rnd(*shape, scale=1.0, dtype=torch.bfloat16):
 
 shapes = {"qkv": (2304, 768, False, 0), "proj": (768, 768, True, 0), "fc1": (3072, 768, False, 1),
           "fc2": (768, 3072, True, 0)}
+if "--with-nogelu" in sys.argv:
+    shapes["fc1_nogelu"] = (3072, 768, False, 0)
 bufs = {}
 for name, (n, k, f32, act) in shapes.items():
     bufs[name] = (rnd(M, k), rnd(n, k, scale=0.05), rnd(n, scale=0.1, dtype=torch.float32),

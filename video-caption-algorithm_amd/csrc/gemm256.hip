@@ -326,12 +326,9 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
           float amax = 0.f;
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            v[j] = acc[qm][qn][i][j] + bias[j];
+            v[j] = gelu_tanh4(acc[qm][qn][i][j] + bias[j]);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              v[j][e] = gelu_tanh(v[j][e]);
-              amax = fmaxf(amax, fabsf(v[j][e]));
-            }
+            for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fabsf(v[j][e]));
           }
           amax = rows_max(amax);
           const int sbyte = mx_scale_byte(amax);
@@ -374,10 +371,7 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             f32x4 v = acc[qm][qn][i][j] + bias[j];
-            if constexpr (EPI == 1) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
-            }
+            if constexpr (EPI == 1) v = gelu_tanh4(v);
             p[j][0] = pack_bf2(v.x, v.y);
             p[j][1] = pack_bf2(v.z, v.w);
           }

@@ -52,6 +52,34 @@ VCAP_DEV float gelu_tanh(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
+// The same GELU on 4 lanes' worth of a GEMM epilogue vector: the polynomial, the +1 and the
+// final product as packed-f32 VALU ops (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32, two
+// elements per instruction), only v_exp_f32 / v_rcp_f32 per element.  Same operations in the
+// same order per element as gelu_tanh (fma contraction included), so the results are identical.
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+VCAP_DEV f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+VCAP_DEV f32x4 gelu_tanh4(f32x4 v) {
+  const float a0 = -2.0f * 1.4426950408889634f * 0.7978845608028654f;
+  const float a1 = a0 * 0.044715f;
+  f32x4 out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f32x2 x = h ? (f32x2){v.z, v.w} : (f32x2){v.x, v.y};
+    const f32x2 t = pk_fma((f32x2){a1, a1}, x * x, (f32x2){a0, a0});
+    const f32x2 y = x * t;
+    const f32x2 d = (f32x2){1.0f, 1.0f} + (f32x2){__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+    const f32x2 r = x * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    if (h) {
+      out.z = r.x;
+      out.w = r.y;
+    } else {
+      out.x = r.x;
+      out.y = r.y;
+    }
+  }
+  return out;
+}
+
 // Cross-lane reductions on the VALU: DPP within 16-lane rows, then the gfx950 permlane16/32
 // swaps across rows.  (__shfl_xor lowers to ds_bpermute, an LDS round trip of ~100+ cycles per
 // step; a 6-step butterfly of those serialises ~700 cycles per reduction.)

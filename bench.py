@@ -7,8 +7,12 @@ frames already resident in HBM: fused ViT encode + engine prefix + mapper (vcap_
 then the whole 24-token greedy decode with the reference generate()'s processors
 (repetition_penalty 1.1, no_repeat_ngram 3, min_new_tokens 8; text_decoder.py:131-144) as
 one replayed hipGraph (vcap_gpt2_generate).  For N>1 (torchrun, one rank per GPU) every rank
-encodes + decodes its own 8 videos (weak scaling, configs[2]) and the int32 token ids are
-gathered with one RCCL all_gather_into_tensor per step - the only collective.
+encodes + decodes its own 8 videos (weak scaling, configs[2]); each batch's int32 token ids are
+copied into a per-run buffer on their decode lane, and the buffer is gathered to every rank with
+ONE RCCL all_gather_into_tensor at the end of the timed region - the only collective.  (A
+collective per batch, issued from the decode lanes, hands work between the lanes and RCCL's
+stream and serialised the two-lane pipeline in a one-GPU rehearsal:
+profiles/r01_gather_topology.txt.)
 
 Rank 0 prints ONE JSON line.  `roofline` is priced on the dominant kernel (the ViT fc1 GEMM,
 `vcap_gemm_kernel<bf16,bf16,1>`), timed live with HIP events around each of its launches in
@@ -128,10 +132,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # VCAP_BENCH_DIST_BACKEND=gloo + ranks sharing GPUs (local % device count): a rehearsal of the
+    # N>1 path on a one-GPU box; the driver's multi-GPU runs use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("VCAP_BENCH_DIST_BACKEND", "nccl")
+    gpu = local % max(torch.cuda.device_count(), 1)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     va, ga = configs.vit_arch(args.vit), configs.gpt2_arch(args.gpt2)
@@ -149,8 +160,15 @@ def main():
     else:
         cfg = GenConfig.raw_greedy(args.max_new, ga.eos_token_id, not args.no_graph)
     cfg.max_blocks = 0 if args.serial else args.decode_blocks
-    gather = (lambda ids: gather_ids(ids, world)) if world > 1 else None
-    pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev, gather=gather,
+    # every batch's ids -> row `slot_of[0]` of a per-run buffer, on the batch's own decode lane
+    ids_all = torch.zeros(max(args.steps, 1), B, args.max_new, dtype=torch.int32, device=dev)
+    slot_of = [0]
+
+    def keep(ids):
+        ids_all[slot_of[0]].copy_(ids)
+        return ids
+
+    pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev, gather=keep if world > 1 else None,
                            reserve_cus=0 if args.serial else args.reserve_cus,
                            dec_lanes=1 if args.serial else args.dec_lanes,
                            confine_decode=args.confine_decode and not args.serial)
@@ -165,6 +183,8 @@ def main():
     pipe.synchronize()
     torch.cuda.synchronize(dev)
     if world > 1:
+        gather_ids(ids_all, world)  # communicator set-up outside the timed region
+        torch.cuda.synchronize(dev)
         dist.barrier()
     lib = N.lib()
     fc1_launches = va.depth * args.steps
@@ -178,8 +198,11 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
+        slot_of[0] = k
         step(starts[k], mids[k], ends[k])
     pipe.synchronize()
+    if world > 1:
+        gathered = gather_ids(ids_all, world)  # [world * steps, B, max_new] on every rank
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -198,7 +221,9 @@ def main():
             # the pipeline's external CU-masked stream that close() destroys); the encode waits on it
             vid_h.copy_(pinned, non_blocking=True)
             pipe.s_enc.wait_stream(torch.cuda.current_stream(dev))
-            ids_host = pipe.result(pipe.submit(vid_h)).cpu()
+            slot_of[0] = 0
+            ids_dev = pipe.result(pipe.submit(vid_h))
+            ids_host = (gather_ids(ids_dev, world) if world > 1 else ids_dev).cpu()
             host_lat.append(time.perf_counter() - t_h)
         host_lat = host_lat[1:]
         torch.cuda.synchronize(dev)

@@ -26,6 +26,8 @@ def gather_ids(local: torch.Tensor, world: int, group=None) -> torch.Tensor:
         out = torch.empty(world * local.shape[0], *local.shape[1:], dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(out, local.contiguous(), group=group)
         return out
-    parts = [torch.empty_like(local) for _ in range(world)]
-    dist.all_gather(parts, local.contiguous(), group=group)
-    return torch.cat(parts, dim=0)
+    # gloo (CPU tests, one-GPU rehearsals): gather host copies
+    host = local.detach().to("cpu").contiguous()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host, group=group)
+    return torch.cat(parts, dim=0).to(local.device)

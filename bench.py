@@ -229,6 +229,11 @@ def main():
         torch.cuda.synchronize(dev)
         del ids_host, pinned, vid_h
 
+    # caption lengths of the last timed batch (new tokens up to and including EOS)
+    last = pipe.result((pipe.k - 1) % pipe.depth).cpu()
+    eos = ga.eos_token_id
+    lens = [int((row == eos).nonzero()[0, 0]) + 1 if bool((row == eos).any()) else int(row.numel()) for row in last]
+
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -276,6 +281,8 @@ def main():
                        f"(batches k..k+{args.dec_lanes - 1}, one HIP stream + graph each; encode CU-masked off "
                        f"{args.reserve_cus} CUs)"},
             "p50_latency_ms": p50,
+            "new_tokens_per_caption": {"mean": sum(lens) / len(lens), "max": max(lens),
+                                       "decode_steps_run": args.max_new},
             "stage_ms_p50": {"vit_encode_prefix": statistics.median(vit_ms),
                              "prefix_ready_to_ids": statistics.median(dec_ms)},
             "roofline": {"bound": "mfma",

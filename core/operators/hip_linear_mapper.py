@@ -3,7 +3,9 @@
 Same parameter names (weight/bias) for checkpoint compatibility and the same bookkeeping
 attributes (`last_backend`, `last_error`).  CUDA inputs run vcap_linear_bias (fp32, or bf16 with
 fp32 accumulation when force_bf16); a failing HIP call raises (strict=True, the default) instead
-of silently falling back.  CPU tensors use torch (they cannot reach the GPU kernel).
+of silently falling back, and so does a CPU input.  torch's Linear runs only when asked for:
+enabled=False, strict=False, or autograd (training / requires_grad - the HIP op has no backward,
+and training is outside this path).
 """
 from __future__ import annotations
 
@@ -24,6 +26,9 @@ class HipLinearCompat(nn.Linear):
         return self.enabled and x.is_cuda and not self.training and not x.requires_grad
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.enabled and self.strict and not x.is_cuda and not (self.training or x.requires_grad):
+            raise RuntimeError("HipLinearCompat: the HIP path needs a GPU tensor (strict=True); "
+                               "use enabled=False or strict=False for torch's Linear")
         if not self._use_hip(x):
             self.last_backend, self.last_error = "torch", ""
             return super().forward(x)

@@ -119,3 +119,16 @@ def test_gather_ids_gloo_world2():
         p.join(timeout=60)
     want = [[0, 1, 2], [3, 4, 5], [100, 101, 102], [103, 104, 105]]
     assert res[0] == want and res[1] == want
+
+
+def test_hip_linear_compat_refuses_cpu_input_when_strict():
+    """No silent CPU fallback on the product path: a CPU tensor through the strict (default)
+    HipLinearCompat raises; torch's Linear runs only when asked for (strict=False / disabled)."""
+    import pytest
+    import torch
+    from core.operators.hip_linear_mapper import HipLinearCompat
+    m = HipLinearCompat(4, 3).eval()
+    with pytest.raises(RuntimeError, match="needs a GPU tensor"):
+        m(torch.zeros(2, 4))
+    loose = HipLinearCompat(4, 3, strict=False).eval()
+    assert loose(torch.zeros(2, 4)).shape == (2, 3) and loose.last_backend == "torch"

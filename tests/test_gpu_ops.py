@@ -176,3 +176,19 @@ def test_abi_errors_are_reported(device):
                        _stream())
     assert rc != 0 and b"K" in lib.vcap_last_error()
     assert lib.vcap_vit_attention(N.DT_F32, 1, 1, 1, 300, 1, _stream()) != 0
+
+
+@pytest.mark.parametrize("M,K", [(25216, 768), (25216, 3072), (20000, 3072)])
+def test_gemm_inplace_residual_auto_policy(device, M, K):
+    """attn-proj / fc2 shapes under the auto policy: whole 256x256 rounds plus the split-K
+    remainder (partials + reduce) - bf16 operands, f32 residual stream updated in place."""
+    N_ = 768
+    N.check(N.lib().vcap_set_gemm_policy(0), "policy")
+    A = _rand((M, K), 21).to(torch.bfloat16)
+    W = _rand((N_, K), 22, 0.03).to(torch.bfloat16)
+    b = _rand((N_,), 23, 0.1)
+    x = _rand((M, N_), 24)
+    ref = x + A.float() @ W.float().t() + b
+    N.check(N.lib().vcap_gemm(N.DT_BF16, N.DT_F32, A.data_ptr(), K, W.data_ptr(), K, x.data_ptr(), N_, M, N_, K,
+                              b.data_ptr(), 0, x.data_ptr(), N_, 1, 0, 0, 0, 0, _stream()), "gemm resid")
+    torch.testing.assert_close(x, ref, rtol=1e-4, atol=2e-4)   # f32 accumulation of bf16 products

@@ -10,6 +10,8 @@ from vcap.model import GenConfig, HipGPT2Decoder
 ga = configs.gpt2_arch("gpt2")
 dev = torch.device("cuda:0")
 dec = HipGPT2Decoder(weights.synthetic_gpt2(1, ga), ga, "bf16", dev)
+from vcap import _native as N
+N.check(N.lib().vcap_set_gemm_policy(int(os.environ.get("VCAP_GEMM_POLICY", "0"))), "policy")
 s = torch.cuda.Stream()
 B = int(os.environ.get("B", "8"))
 with torch.cuda.stream(s):
@@ -25,4 +27,4 @@ with torch.cuda.stream(s):
             dec.generate_ids(pre, [50256], cfg)
         torch.cuda.synchronize()
         res[mx] = (time.perf_counter() - t) / 10 * 1e3
-print(f"{Path(os.environ.get('VCAP_LIB', 'base')).name}: B={B} step {(res[24]-res[1])/23*1e3:.1f} us prefill {res[1]*1e3:.0f} us")
+print(f"{Path(os.environ.get('VCAP_LIB', 'base')).name} policy {os.environ.get('VCAP_GEMM_POLICY', '0')}: B={B} step {(res[24]-res[1])/23*1e3:.1f} us prefill {res[1]*1e3:.0f} us")

@@ -319,31 +319,36 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
           const int n = min(nb + j * 16 + fg * 4, N - 4);
           bias[j] = *reinterpret_cast<const f32x4*>(epi.bias + n);
         }
+        // rows i and i+1 (16 apart) at a time: after quantisation the 4 lanes of a row hold 4
+        // fp8 of each 16-column half; a 4x4 lane-group transpose gives every lane 16 contiguous
+        // bytes (group 0: row i cols 0-15, 1: row i cols 16-31, 2 / 3: row i+1), one dwordx4
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0 + wr * 128 + qm * 64 + i * 16 + fr;
-          f32x4 v[2];
-          float amax = 0.f;
+        for (int i = 0; i < 4; i += 2) {
+          uint32_t x[4];
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            v[j] = gelu_tanh4(acc[qm][qn][i][j] + bias[j]);
+          for (int h = 0; h < 2; ++h) {
+            const int m = m0 + wr * 128 + qm * 64 + (i + h) * 16 + fr;
+            f32x4 v[2];
+            float amax = 0.f;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fabsf(v[j][e]));
+            for (int j = 0; j < 2; ++j) {
+              v[j] = gelu_tanh4(acc[qm][qn][i + h][j] + bias[j]);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fabsf(v[j][e]));
+            }
+            amax = rows_max(amax);
+            const int sbyte = mx_scale_byte(amax);
+            const float inv = mx_inv_scale(sbyte);
+            const f32x4 q0 = v[0] * inv, q1 = v[1] * inv;
+            x[2 * h] = pack_fp8x4(q0.x, q0.y, q0.z, q0.w);
+            x[2 * h + 1] = pack_fp8x4(q1.x, q1.y, q1.z, q1.w);
+            if (fg == 0 && m < M && nb < N) epi.c_scale[mx_scale_index(m, nb, (M + 255) >> 8)] = (uint8_t)sbyte;
           }
-          amax = rows_max(amax);
-          const int sbyte = mx_scale_byte(amax);
-          const float inv = mx_inv_scale(sbyte);
-          // lanes fg, fg ^ 1 trade halves so each stores 8 contiguous bytes (one dwordx2 instead
-          // of two dword stores): even lane columns [8k, 8k+8) of j = 0, odd [16+8k, +8) of j = 1
-          const bool odd = (lane & 16) != 0;
-          const f32x4 q0 = v[0] * inv, q1 = v[1] * inv;
-          const uint32_t p0 = pack_fp8x4(q0.x, q0.y, q0.z, q0.w), p1 = pack_fp8x4(q1.x, q1.y, q1.z, q1.w);
-          const uint32_t r = (uint32_t)xor16_i((int)(odd ? p0 : p1));
-          if (m < M && nb < N) {
-            *reinterpret_cast<u32x2*>((uint8_t*)C + (long)m * ldc + nb + (odd ? 12 + 4 * fg : 4 * fg)) =
-                odd ? (u32x2){r, p1} : (u32x2){p0, r};
-            if (fg == 0) epi.c_scale[mx_scale_index(m, nb, (M + 255) >> 8)] = (uint8_t)sbyte;
-          }
+          transpose4_groups(x);
+          const int ms = m0 + wr * 128 + qm * 64 + (i + (fg >> 1)) * 16 + fr;
+          if (ms < M && nb < N)
+            *reinterpret_cast<u32x4*>((uint8_t*)C + (long)ms * ldc + nb + (fg & 1) * 16) =
+                (u32x4){x[0], x[1], x[2], x[3]};
         }
       }
   } else if (sizeof(TOut) == 2 && (EPI == 0 || EPI == 1) && (N & 31) == 0 && (ldc & 7) == 0 &&

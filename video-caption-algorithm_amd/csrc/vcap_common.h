@@ -111,6 +111,26 @@ VCAP_DEV int xor32_i(int v) {
   return (int)((threadIdx.x & 32) ? r[0] : r[1]);
 }
 
+// 4x4 transpose of dwords across the lane groups {l, l^16, l^32, l^48} (same position in every
+// 16-lane row): on return, lane group g holds (x[0], x[1], x[2], x[3]) of groups 0, 1, 2, 3 as
+// they were in slot g.  Two butterfly stages, each lane exchanging its "receive" slot of every
+// slot pair with the partner group (v_permlane16_swap, then v_permlane32_swap).
+VCAP_DEV void transpose4_groups(uint32_t (&x)[4]) {
+  const int g = (threadIdx.x >> 4) & 3;
+#pragma unroll
+  for (int base = 0; base < 4; base += 2) {  // stage 1: pairs (0,1), (2,3) with group g ^ 1
+    const bool lo = g & 1;                   // receive slot: the one whose bit 0 differs from g's
+    const uint32_t r = (uint32_t)xor16_i((int)(lo ? x[base] : x[base + 1]));
+    if (lo) x[base] = r; else x[base + 1] = r;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // stage 2: pairs (0,2), (1,3) with group g ^ 2
+    const bool lo = g & 2;
+    const uint32_t r = (uint32_t)xor32_i((int)(lo ? x[k] : x[k + 2]));
+    if (lo) x[k] = r; else x[k + 2] = r;
+  }
+}
+
 VCAP_DEV float row16_sum(float v) {
   v += dpp_f<DPP_XOR1>(v);
   v += dpp_f<DPP_XOR2>(v);

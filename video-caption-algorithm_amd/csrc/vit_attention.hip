@@ -297,7 +297,10 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
     const bool keep = q < N && (!cls_only || q == 0);
     const long row = cls_only ? (long)bt : (long)bt * N + q;
     if constexpr (MXO) {
-      // block b = dims [32b, 32b+32) of row q: dt in {2b, 2b+1} of this lane and lanes fg = 0..3
+      // block b = dims [32b, 32b+32) of row q: dt in {2b, 2b+1} of this lane and lanes fg = 0..3;
+      // after quantisation a 4x4 lane-group transpose hands every lane 16 contiguous bytes of the
+      // head's 64 (lane group g: dims [16g, 16g+16)), one dwordx4 store per lane
+      uint32_t x[4];
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const f32x4 v0 = o[2 * b] * inv, v1 = o[2 * b + 1] * inv;
@@ -307,18 +310,13 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
         amax = rows_max(amax);
         const int sb = mx_scale_byte(amax);
         const float is = mx_inv_scale(sb);
-        // lanes fg, fg ^ 1 trade halves: one 8-byte store each (even: bytes [8k, 8k+8) of the
-        // first 16, odd: [16 + 8k, +8))
-        const bool odd = (threadIdx.x & 16) != 0;
-        const uint32_t p0 = pack_fp8x4(v0.x * is, v0.y * is, v0.z * is, v0.w * is);
-        const uint32_t p1 = pack_fp8x4(v1.x * is, v1.y * is, v1.z * is, v1.w * is);
-        const uint32_t r = (uint32_t)xor16_i((int)(odd ? p0 : p1));
-        if (keep) {
-          uint8_t* orow = (uint8_t*)out + row * D + h * 64 + 32 * b;
-          *reinterpret_cast<u32x2*>(orow + (odd ? 12 + 4 * fg : 4 * fg)) = odd ? (u32x2){r, p1} : (u32x2){p0, r};
-          if (fg == 0) oscale[mx_scale_index((int)row, h * 64 + 32 * b, groups)] = (uint8_t)sb;
-        }
+        x[2 * b] = pack_fp8x4(v0.x * is, v0.y * is, v0.z * is, v0.w * is);
+        x[2 * b + 1] = pack_fp8x4(v1.x * is, v1.y * is, v1.z * is, v1.w * is);
+        if (keep && fg == 0) oscale[mx_scale_index((int)row, h * 64 + 32 * b, groups)] = (uint8_t)sb;
       }
+      transpose4_groups(x);
+      if (keep)
+        *reinterpret_cast<u32x4*>((uint8_t*)out + row * D + h * 64 + 16 * fg) = (u32x4){x[0], x[1], x[2], x[3]};
     } else {
       // O[q][d = dt*16 + 4*fg + r]; lanes fg, fg ^ 1 (lane ^ 16) trade halves of the dt pair
       // (2k, 2k+1) so each stores 8 contiguous dims with one dwordx4 (the even lane dims

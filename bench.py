@@ -117,6 +117,23 @@ def fc1_traffic(M: int, N: int, K: int):
     return float(b["fetch"] + b["write"])
 
 
+def pmc_summary(vit: str, gpt2: str, B: int, T: int, precision: str):
+    """MFMA utilisation of the ViT GEMMs and the decode's HBM bytes per token step from the
+    committed rocprofv3 PMC passes (profiles/r01_pmc.json: tools/pmc.sh + tools/pmc_report.py on
+    this configs[1] workload); None for other workloads (counters cannot be read in bench.py)."""
+    if (vit, gpt2, B, T, precision) != ("vit_base_patch16_224", "gpt2", 8, 16, "bf16"):
+        return None
+    try:
+        d = json.loads((ROOT / "profiles" / "r01_pmc.json").read_text())
+    except (OSError, ValueError):
+        return None
+    util = {k.split("<", 1)[1].rstrip(">"): round(v["mfma_util"], 3) for k, v in d["vit_kernels"].items()
+            if "gemm256" in k and v.get("mfma_util")}
+    return {"source": "profiles/r01_pmc.json (rocprofv3 --pmc, separate passes)",
+            "vit_gemm_mfma_util": util,
+            "decode_hbm_bytes_per_token_step": d["decode"]["hbm_bytes_per_token_step"]}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -306,6 +323,7 @@ def main():
             "path_roofline": {"t_roof_ms": t_roof * 1e3, "t_measured_ms": elapsed / args.steps * 1e3,
                               "frac": t_roof / (elapsed / args.steps),
                               "vit_tflop": vit_exec / 1e12, "decode_weight_gb": dec_bytes / 1e9},
+            "pmc": pmc_summary(args.vit, args.gpt2, B, T, args.precision),
             "vit_flops_per_step": B * T * va.flops_per_frame(),
             "vit_flops_per_step_executed": B * T * va.flops_per_frame(cls_tail=True),
         }

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 5
+#define VCAP_ABI_VERSION 6
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -197,6 +197,16 @@ int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const
                        int prompt_len, int B, int* out_ids, float* logits_out, void* workspace, size_t ws_bytes,
                        void* stream);
 void vcap_graph_cache_clear(void);
+/* number of instantiated decode graphs held by the cache (bounded LRU, VCAP_GRAPH_CACHE_MAX) */
+int vcap_graph_cache_size(void);
+
+/* ---- causal decode attention over the paged KV cache (one GPT-2 layer; HF GPT2Attention's
+ *      sdpa path at decode time, text_decoder.py:131-144 -> modeling_gpt2): q [M, H*64] (M = seqs *
+ *      S_new rows), pools [pages][H][16][64], page_table [seqs][maxp] or NULL for the contiguous
+ *      layout (page of position j of sequence s = s*maxp + j/16), out [M, H*64].  Row m attends
+ *      to positions 0 .. past + (m % S_new) of its sequence. ---- */
+int vcap_decode_attention(int dtype, const void* q, const void* k_pool, const void* v_pool, const int* page_table,
+                          int maxp, void* out, int M, int heads, int S_new, int past, void* stream);
 
 /* ---- step-wise decode for host-driven search (beam search / sampling).  One state carved for
  *      `rows` decoder rows lives in the caller's workspace across calls:

@@ -132,3 +132,39 @@ def test_hip_linear_compat_refuses_cpu_input_when_strict():
         m(torch.zeros(2, 4))
     loose = HipLinearCompat(4, 3, strict=False).eval()
     assert loose(torch.zeros(2, 4)).shape == (2, 3) and loose.last_backend == "torch"
+
+
+class _StubCaptioner:
+    """generate_ids stand-in (CPU): row i's ids derive from that video's content only."""
+    device = torch.device("cpu")
+
+    def generate_ids(self, videos, prompt_ids, ln_scale=0.6, in_weight=0.4, cfg=None):
+        base = videos.reshape(videos.shape[0], -1)[:, 0].round().to(torch.int32)
+        return base[:, None] * 10 + torch.arange(cfg.max_new_tokens, dtype=torch.int32)[None, :]
+
+
+def _sharded_worker(rank, world, port, n, q):
+    from vcap.dist import caption_sharded
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    videos = torch.arange(n, dtype=torch.float32).reshape(n, 1, 1, 1, 1).expand(n, 2, 3, 4, 4).contiguous()
+    from types import SimpleNamespace
+    out = caption_sharded(_StubCaptioner(), videos, [0], cfg=SimpleNamespace(max_new_tokens=5))
+    q.put((rank, out.tolist()))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 5), (3, 7), (3, 2)])
+def test_caption_sharded_gloo(world, n):
+    """Uneven shards (and an empty one) come back in global order on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    want = [[v * 10 + j for j in range(5)] for v in range(n)]
+    assert all(res[r] == want for r in range(world))

@@ -1,0 +1,266 @@
+"""Parity of the BENCHMARKED kernel set (bf16: gemm256<bf16>, the bf16 ViT attention, the CLS-tail
+split-K, the bf16 rows GEMVs, decode_attention_c64, the lm_head processor epilogue) against the
+reference's recorded outputs (tests/golden/b16_b8 = BASELINE configs[1], produced by running the
+reference's own generate(): tests/golden/make_goldens.py) and against fp32 torch references at
+the bench shapes.
+
+Tolerances (bf16 operands, fp32 accumulation): teacher-forced step logits within BF16_LOGIT_TOL of
+the reference's fp32 logits at every one of the 24 steps; greedy tokens identical wherever the
+reference's processed top-2 gap exceeds that tolerance; free-running token agreement above a
+stated floor (bf16 rounding flips near-ties, after which a greedy continuation legitimately
+diverges - the fp32 mode is the token-exact one, tests/test_gpu_parity.py)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import case
+from vcap import _native as N
+from vcap import search
+from vcap.caption import HipGPT2LMHead, _WTE
+from vcap.model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, trim_generated
+
+pytestmark = pytest.mark.gpu
+
+BF16_LOGIT_TOL = 0.02          # |bf16 HIP - fp32 reference| on every raw logit the golden records (measured max 0.013)
+FREE_RUN_PREFIX_FLOOR = 0.9    # mean fraction of each caption's leading tokens equal to the reference's (measured 1.0)
+_CACHE = {}
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _models(prec, device, name="b16_b8"):
+    meta, g, va, ga, sd, frames = case(name)
+    key = (name, prec)
+    if key not in _CACHE:
+        _CACHE.clear()
+        _CACHE[key] = (HipViTEncoder(sd, va, prec, device), HipPrefix(sd, ga.n_embd, device=device),
+                       HipGPT2Decoder(sd, ga, prec, device))
+    return (meta, g, va, ga, sd, frames) + _CACHE[key]
+
+
+def _hf_cfg(ga, graph=True, max_blocks=0):
+    c = GenConfig(24, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, graph)
+    c.max_blocks = max_blocks
+    return c
+
+
+def _golden_step(g, s):
+    return g[f"hf_greedy_logits_s{s}_top_i"].astype(np.int64), g[f"hf_greedy_logits_s{s}_top_v"]
+
+
+def _processed_top2_gap(ti, tv, hist, V, eos, step):
+    """Processed (rep 1.1, ngram 3, min_new 8) top-2 gap of the golden raw logits, computed on the
+    golden top-64 (every other logit set far below): rows whose gap is certain."""
+    row = torch.full((ti.shape[0], V), -1e30, dtype=torch.float64)
+    row.scatter_(1, torch.from_numpy(ti), torch.from_numpy(tv.astype(np.float64)))
+    sc = search._processors(row, torch.from_numpy(hist.astype(np.int64)), 1.1, 3, 8, eos)
+    top = torch.topk(sc, 2, dim=-1).values
+    return (top[:, 0] - top[:, 1]).numpy(), sc.argmax(-1).numpy()
+
+
+def test_bf16_teacher_forced_all_steps(device):
+    """bf16 decoder fed the reference's fp32 prefix and, at each step, the reference's own greedy
+    token (fp32 wte rows): every step's raw logits within BF16_LOGIT_TOL of the reference's, and
+    the processed argmax identical wherever the reference's processed top-2 gap > the tolerance."""
+    meta, g, va, ga, sd, frames, enc, pre, dec = _models("bf16", device)
+    B, V, eos = meta["B"], ga.vocab, ga.eos_token_id
+    steps = meta["hf_greedy_logit_steps"]
+    assert steps == 24
+    ids = g["hf_greedy_ids"]
+    wte32 = torch.from_numpy(sd["decoder.model.transformer.wte.weight"]).to(device)
+    lm = HipGPT2LMHead(dec, ga, _WTE(dec.wte))
+    x = torch.from_numpy(g["inputs_embeds"].copy()).to(device)    # [B, 5, E] fp32 (prefix + BOS)
+    out = lm(inputs_embeds=x, use_cache=True)
+    errs, checked, flips = [], 0, []
+    for s in range(steps):
+        lg = out.logits[:, -1, :].double()
+        ti, tv = _golden_step(g, s)
+        got = torch.gather(lg, 1, torch.from_numpy(ti).to(device)).cpu().numpy()
+        errs.append(float(np.abs(got - tv).max()))
+        gap, gold_arg = _processed_top2_gap(ti, tv, ids[:, :s], V, eos, s)
+        assert np.array_equal(gold_arg, ids[:, s]), "golden top-64 does not reproduce the golden token"
+        mine = search._processors(lg, torch.from_numpy(ids[:, :s].astype(np.int64)).to(device), 1.1, 3, 8, eos)
+        mine = mine.argmax(-1).cpu().numpy()
+        sure = gap > BF16_LOGIT_TOL
+        checked += int(sure.sum())
+        flips += [(s, int(b)) for b in np.nonzero(sure & (mine != ids[:, s]))[0]]
+        if s + 1 < steps:
+            emb = wte32[torch.from_numpy(ids[:, s].astype(np.int64)).to(device)].unsqueeze(1)
+            out = lm(inputs_embeds=emb, past_key_values=out.past_key_values, use_cache=True)
+    print(f"bf16 teacher-forced: max |dlogit| per step {np.round(errs, 4).tolist()}; "
+          f"{checked} of {B * steps} tokens certain, flips {flips}")
+    assert max(errs) < BF16_LOGIT_TOL, errs
+    assert not flips, flips
+    assert checked >= 0.75 * B * steps
+
+
+def _free_running(device):
+    meta, g, va, ga, sd, frames, enc, pre, dec = _models("bf16", device)
+    _, prefix = enc.encode(torch.from_numpy(frames).to(device), pre)
+    ids = dec.generate_ids(prefix, [ga.bos_token_id], _hf_cfg(ga)).cpu().numpy()
+    return ids, g["hf_greedy_ids"]
+
+
+def token_agreement(got, ref):
+    """(mean leading-token agreement per caption, position-wise agreement) of [B, L] id arrays."""
+    lead = []
+    for a, b in zip(got, ref):
+        n = 0
+        while n < len(b) and n < len(a) and a[n] == b[n]:
+            n += 1
+        lead.append(n / len(b))
+    return float(np.mean(lead)), float((got[:, :ref.shape[1]] == ref).mean())
+
+
+def test_bf16_free_running_agreement(device):
+    """The benchmark's bf16 path end to end (encode + fused greedy decode graph) against the
+    reference's HF-greedy captions of the same 8 videos."""
+    got, ref = _free_running(device)
+    lead, pos = token_agreement(got, ref)
+    print(f"bf16 free-running: leading-token agreement {lead:.3f}, position-wise {pos:.3f}")
+    assert lead >= FREE_RUN_PREFIX_FLOOR, (lead, got, ref)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_lm_head_processor_epilogue_every_step(device, prec):
+    """The lm_head epilogue (RepetitionPenalty -> NoRepeatNGram -> MinNewTokens -> argmax partials)
+    + finalize, all 24 steps: the token each step emits equals torch's processors + argmax
+    applied to the raw logits the same kernel wrote (integer-exact)."""
+    meta, g, va, ga, sd, frames, enc, pre, dec = _models(prec, device)
+    B, eos = meta["B"], ga.eos_token_id
+    prefix = torch.from_numpy(g["inputs_embeds"][:, :4].copy()).to(device)
+    logits = torch.empty(24, B, ga.vocab, device=device)
+    ids = dec.generate_ids(prefix, [ga.bos_token_id], _hf_cfg(ga, graph=False), logits_out=logits)
+    ids64 = ids.long()
+    fin = torch.zeros(B, dtype=torch.bool, device=device)
+    for s in range(24):
+        sc = search._processors(logits[s], ids64[:, :s], 1.1, 3, 8, eos)
+        exp = torch.where(fin, torch.full_like(ids64[:, s], eos), sc.argmax(-1))
+        assert torch.equal(exp, ids64[:, s]), (s, exp, ids64[:, s])
+        fin |= ids64[:, s] == eos
+
+
+def test_bf16_pipeline_bit_identical_to_serial(device):
+    """The bench schedule (vcap/pipeline.py: CU-masked encode stream, two decode lanes with capped
+    grids, own workspaces / graphs) gives bit-identical bf16 encodes and ids to a serial bf16
+    encode + generate_ids on the default stream (deterministic split-K, mask-independent plans)."""
+    from vcap.pipeline import CaptionPipeline
+    meta, g, va, ga, sd, frames, enc, pre, dec = _models("bf16", device)
+    video = torch.from_numpy(frames).to(device)
+    emb_serial, pre_serial = enc.encode(video, pre)
+    ids_serial = dec.generate_ids(pre_serial, [ga.bos_token_id], _hf_cfg(ga)).clone()
+    cfg = _hf_cfg(ga, max_blocks=128)
+    pipe = CaptionPipeline(enc, pre, dec, cfg, video.shape[0], [ga.bos_token_id], device, reserve_cus=32,
+                           dec_lanes=2)
+    try:
+        slots = [pipe.submit(video) for _ in range(5)]
+        for slot in slots[-3:]:
+            assert torch.equal(pipe.result(slot), ids_serial)
+            assert torch.equal(pipe.prefix_bufs[slot], pre_serial)
+    finally:
+        pipe.close()
+
+
+# ------------------------------------------------------------------ per-kernel tests at bench shapes
+
+def _rand(shape, seed, scale=1.0, device="cuda"):
+    gen = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=gen) * scale).to(device)
+
+
+M_BENCH = 8 * 16 * 197   # configs[1]: 8 videos x 16 frames x 197 tokens = 25216 rows
+
+
+@pytest.mark.parametrize("role,N_,K,act", [("qkv", 2304, 768, 0), ("fc1", 3072, 768, 1)])
+def test_gemm_bench_shape_bf16_out(device, role, N_, K, act):
+    """QKV (bias) and fc1 (bias + tanh-GELU) at M = 25216 under the auto policy (256x256 rounds +
+    128x128 remainder), bf16 out, against fp32 torch on the same bf16 operands."""
+    N.check(N.lib().vcap_set_gemm_policy(0), "policy")
+    A = _rand((M_BENCH, K), 31).to(torch.bfloat16)
+    W = _rand((N_, K), 32, 0.03).to(torch.bfloat16)
+    b = _rand((N_,), 33, 0.1)
+    out = torch.empty(M_BENCH, N_, dtype=torch.bfloat16, device=device)
+    N.check(N.lib().vcap_gemm(N.DT_BF16, N.DT_BF16, A.data_ptr(), K, W.data_ptr(), K, out.data_ptr(), N_, M_BENCH, N_,
+                              K, b.data_ptr(), act, None, 0, 0, 0, 0, 0, 0, _stream()), role)
+    ref = A.float() @ W.float().t() + b
+    if act:
+        ref = F.gelu(ref, approximate="tanh")
+    # one bf16 rounding of an fp32-accumulated value: <= 2^-8 relative (+ summation order)
+    torch.testing.assert_close(out.float(), ref, rtol=8e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("N_,K", [(2304, 768), (768, 3072)])
+def test_gemm_tile128_and_tile256_bitwise_equal(device, N_, K):
+    """The 128x128 and 256x256 kernels issue the same MFMA chain per output (K ascending, weight
+    fragment as operand A): the dispatcher's whole-round / remainder split, which depends on the
+    stream's CU mask, therefore cannot change a single bit of the encode."""
+    M = 4096
+    A = _rand((M, K), 34).to(torch.bfloat16)
+    W = _rand((N_, K), 35, 0.03).to(torch.bfloat16)
+    b = _rand((N_,), 36, 0.1)
+    outs = []
+    for pol in (1, 2):
+        N.check(N.lib().vcap_set_gemm_policy(pol), "policy")
+        x = _rand((M, N_), 37)
+        N.check(N.lib().vcap_gemm(N.DT_BF16, N.DT_F32, A.data_ptr(), K, W.data_ptr(), K, x.data_ptr(), N_, M, N_, K,
+                                  b.data_ptr(), 0, x.data_ptr(), N_, 1, 0, 0, 0, 0, _stream()), "gemm")
+        outs.append(x)
+    N.check(N.lib().vcap_set_gemm_policy(0), "policy")
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_vit_attention_bench_shape_bf16(device):
+    """128 frames x 12 heads x 197 tokens (configs[1]) against fp32 SDPA on the same bf16 q/k/v."""
+    BT, Ntok, H = 128, 197, 12
+    D = H * 64
+    qkv = _rand((BT * Ntok, 3 * D), 38, 1.5).to(torch.bfloat16)
+    out = torch.empty(BT * Ntok, D, dtype=torch.bfloat16, device=device)
+    N.check(N.lib().vcap_vit_attention(N.DT_BF16, qkv.data_ptr(), out.data_ptr(), BT, Ntok, H, _stream()), "attn")
+    q, k, v = qkv.float().reshape(BT, Ntok, 3, H, 64).permute(2, 0, 3, 1, 4).unbind(0)
+    ref = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(BT * Ntok, D)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def _decode_attn_ref(q, kc, vc, pt, maxp, H, S_new, past):
+    M = q.shape[0]
+    out = torch.empty(M, H * 64, device=q.device)
+    for m in range(M):
+        seq, qpos = m // S_new, past + m % S_new
+        pos = torch.arange(qpos + 1, device=q.device)
+        pages = pt[seq, pos // 16].long() if pt is not None else seq * maxp + pos // 16
+        kk = kc.float()[pages, :, pos % 16]   # [ctx, H, 64]
+        vv = vc.float()[pages, :, pos % 16]
+        qq = q.float()[m].reshape(H, 64)
+        att = torch.einsum("hd,chd->hc", qq, kk) / 8.0
+        out[m] = torch.einsum("hc,chd->hd", att.softmax(-1), vv).reshape(-1)
+    return out
+
+
+@pytest.mark.parametrize("prec,S_new,past,paged", [("bf16", 1, 28, False), ("bf16", 5, 0, False),
+                                                   ("bf16", 1, 63, False), ("bf16", 1, 70, True),
+                                                   ("fp32", 1, 28, True), ("fp32", 5, 0, True)])
+def test_decode_attention(device, prec, S_new, past, paged):
+    """vcap_decode_attention: the bf16 contiguous-page fast path (decode_attention_c64, context
+    <= 64: every configs[1] step) and the page-table kernel, against an fp32 torch reference."""
+    tdt = torch.bfloat16 if prec == "bf16" else torch.float32
+    dt = N.DT_BF16 if prec == "bf16" else N.DT_F32
+    seqs, H = 8, 12
+    ctx = past + S_new
+    maxp = (ctx + 15) // 16 + 1
+    M = seqs * S_new
+    q = _rand((M, H * 64), 40).to(tdt)
+    kc = _rand((seqs * maxp, H, 16, 64), 41).to(tdt)
+    vc = _rand((seqs * maxp, H, 16, 64), 42).to(tdt)
+    pt = None
+    if paged:   # a shuffled page table
+        perm = torch.randperm(seqs * maxp, generator=torch.Generator().manual_seed(43)).int()
+        pt = perm.reshape(seqs, maxp).to(device)
+    out = torch.empty(M, H * 64, dtype=tdt, device=device)
+    N.check(N.lib().vcap_decode_attention(dt, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), N.ptr(pt), maxp,
+                                          out.data_ptr(), M, H, S_new, past, _stream()), "decode attention")
+    ref = _decode_attn_ref(q, kc, vc, pt, maxp, H, S_new, past)
+    tol = 1e-2 if prec == "bf16" else 1e-5
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)

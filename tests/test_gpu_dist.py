@@ -1,0 +1,51 @@
+"""Multi-GPU product path: vcap.dist.caption_sharded run by 2 fresh child ranks
+(one process per rank, gloo, both on the box's one GPU) gives the single-process reference ids.
+tiny_prompt has B = 3 videos: shards of 2 and 1 exercise the padded gather."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from helpers import golden, pad_rows
+from vcap.model import trim_generated  # noqa: F401  (import check)
+
+pytestmark = pytest.mark.gpu
+HERE = Path(__file__).resolve().parent
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("name", ["tiny_prompt", "tiny"])
+def test_caption_sharded_two_ranks_match_goldens(tmp_path, name):
+    out = tmp_path / "ids.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2")
+    procs = [subprocess.Popen([sys.executable, str(HERE / "dist_worker.py"), name, str(out)],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=100)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("a rank hung")
+    assert all(p.returncode == 0 for p in procs), "\n".join(l[-3000:] for l in logs)
+    res = json.loads(out.read_text())
+    meta, g = golden(name)
+    got = np.array(res["ids"], dtype=np.int32)
+    exp = g["hf_greedy_ids"]
+    eos = 50256 if meta["gpt2"] == "gpt2" else 1023
+    # generate_ids is EOS-padded to max_new; the golden stops where every row has finished
+    assert res["world"] == 2 and got.shape[0] == meta["B"]
+    assert np.array_equal(got[:, :exp.shape[1]], exp)
+    assert (got[:, exp.shape[1]:] == eos).all()

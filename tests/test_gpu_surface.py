@@ -1,0 +1,125 @@
+"""Engine-level parity: the drop-in surface (core.engine.InferenceEngine, VideoCaptionModel.generate,
+the sampling presets) against outputs recorded by running the reference's own engine
+(tests/golden/make_goldens.py `surface_case`: core/engine.py:39-83, src/models/caption_model.py:93-101,
+HF generate's processed sampling scores).  fp32 mode (the token-exact one)."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import case, golden
+from vcap import _native as N
+from vcap import search
+from vcap.model import trim_generated
+
+pytestmark = pytest.mark.gpu
+
+GREEDY = dict(num_beams=1, max_new_tokens=24, temperature=1.0, top_p=1.0, no_repeat_ngram_size=3,
+              repetition_penalty=1.1)
+_ENG = {}
+
+
+def _engine(name, device):
+    from core.config import InferenceConfig
+    from core.engine import InferenceEngine
+    meta, g, va, ga, sd, frames = case(name)
+    surf = meta["surface"]
+    if name not in _ENG:
+        _ENG.clear()
+        cfg = InferenceConfig(vit_name=meta["vit"], gpt2_name=meta["gpt2"], num_frames=meta["T"], precision="fp32",
+                              device=str(device), weights_seed=meta["weights_seed"], preset1="precise",
+                              preset2="precise", preset3="natural", prompt1="", prompt2=surf["prompt_text"],
+                              prompt3=surf["prompt_text"])
+        _ENG[name] = InferenceEngine(cfg)
+    return meta, g, ga, surf, _ENG[name], torch.from_numpy(frames).to(device)
+
+
+@pytest.mark.parametrize("name", ["tiny", "b16_b2"])
+def test_generate_once_greedy_and_precise(device, name):
+    """_generate_once strings (decode -> batch_decode -> clean_text) and the ids behind them."""
+    from core.inference import preset_to_kwargs
+    meta, g, ga, surf, eng, video = _engine(name, device)
+    assert eng._generate_once(video, "", **GREEDY) == surf["greedy_text"]
+    assert eng._generate_once(video, "", **preset_to_kwargs("precise")) == surf["precise_text"]
+    assert eng._generate_once(video, surf["prompt_text"], **GREEDY) == surf["prompt_greedy_text"]
+    dec, prefix = eng.model.decoder, eng._prefix(video)
+    bos = [ga.bos_token_id]
+    assert dec.generate_from_prefix(prefix, bos, **GREEDY, min_new_tokens=8) == g["hf_greedy_ids"].tolist()
+    assert dec.generate_from_prefix(prefix, bos, **preset_to_kwargs("precise"), min_new_tokens=8) == surf["precise_ids"]
+    pids = dec.tokenizer.encode_prompt(surf["prompt_text"])
+    assert dec.generate_from_prefix(prefix, pids, **GREEDY, min_new_tokens=8) == surf["prompt_greedy_ids"]
+    assert dec.generate_from_prefix(prefix, pids, **preset_to_kwargs("precise"), min_new_tokens=8) == \
+        surf["prompt_precise_ids"]
+
+
+@pytest.mark.parametrize("name", ["tiny", "b16_b2"])
+def test_infer_candidates_s1_s2(device, name):
+    """infer() (core/engine.py:66-83): S1 = precise + prompt1, S2 = precise + prompt2 equal the
+    reference engine's strings (S3 samples: its parity is the distributional test below)."""
+    meta, g, ga, surf, eng, video = _engine(name, device)
+    res = eng.infer_video(video)
+    assert res.candidates.s1 == surf["precise_text"]
+    assert res.candidates.s2 == surf["prompt_precise_text"]
+    assert res.best_key in {"S1", "S2", "S3"}
+
+
+@pytest.mark.parametrize("name", ["tiny", "b16_b2"])
+def test_video_caption_model_generate_no_ln_scale(device, name):
+    """VideoCaptionModel.generate: encoder -> proj -> decoder.generate WITHOUT the engine's LN-scale
+    (src/models/caption_model.py:93-101): every row's text equals the reference's."""
+    meta, g, ga, surf, eng, video = _engine(name, device)
+    texts = eng.model.generate(video, prompt="", **GREEDY)
+    assert texts == surf["model_generate_texts"]
+
+
+def test_repeated_generate_once_reuses_one_graph(device):
+    """50 engine calls with fresh prefix tensors each time: the decode graph cache stays at one
+    entry per shape (persistent decode buffers + bounded LRU)."""
+    meta, g, ga, surf, eng, video = _engine("tiny", device)
+    N.lib().vcap_graph_cache_clear()
+    for _ in range(50):
+        eng._generate_once(video, "", **GREEDY)
+    torch.cuda.synchronize()
+    assert N.lib().vcap_graph_cache_size() == 1
+
+
+@pytest.mark.parametrize("preset", ["natural", "safe_sample"])
+def test_sampling_scores_match_hf_warpers(device, preset):
+    """The distribution `natural` / `safe_sample` draw from: HIP-side processors + Temperature +
+    TopP applied to the reference's raw logits with the reference's sampled history equal HF's
+    processed scores (same -inf mask, finite scores within 1e-5), every step."""
+    meta, g = golden("tiny")
+    kw = meta[preset]
+    logits = torch.from_numpy(g[f"{preset}_logits"]).to(device)    # [steps, B, V]
+    scores = torch.from_numpy(g[f"{preset}_scores"]).to(device)
+    ids = torch.from_numpy(g[f"{preset}_ids"].astype(np.int64)).to(device)
+    for s in range(logits.shape[0]):
+        got = search.sampling_scores(logits[s], ids[:, :s], temperature=kw["temperature"], top_p=kw["top_p"],
+                                     rep=kw["repetition_penalty"], ngram=kw["no_repeat_ngram_size"],
+                                     min_new=kw["min_new_tokens"], eos=1023)
+        fin = torch.isfinite(scores[s])
+        assert torch.equal(torch.isfinite(got), fin), s
+        torch.testing.assert_close(got[fin], scores[s][fin], rtol=1e-5, atol=1e-5)
+
+
+def test_checkpoint_roundtrip(device, tmp_path):
+    """A reference-format checkpoint ({"model_state": state_dict}, src/cli/train_caption_mapper.py:301-305)
+    loaded through load_caption_model(ckpt=...) (model_loader.py:31-80) decodes the golden ids;
+    keys missing from the checkpoint follow the reference's strict=False (logged, kept at init)."""
+    from core.config import InferenceConfig
+    from core.models.model_loader import load_caption_model
+    meta, g, va, ga, sd, frames = case("tiny")
+    ck = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()}
+    path = tmp_path / "ckpt.pt"
+    torch.save({"model_state": ck, "step": 1, "epoch": 0}, path)
+    cfg = InferenceConfig(ckpt=str(path), vit_name=meta["vit"], gpt2_name=meta["gpt2"], num_frames=meta["T"],
+                          precision="fp32", device=str(device), weights_seed=meta["weights_seed"])
+    m = load_caption_model(cfg)
+    ids = m.generate_ids(torch.from_numpy(frames).to(device), [ga.bos_token_id])
+    assert trim_generated(ids, ga.eos_token_id) == g["hf_greedy_ids"].tolist()
+    # strict=False: drop a key -> it keeps the initialiser's value (seeded init = the same weights here)
+    ck2 = dict(ck)
+    ck2.pop("encoder.proj.bias")
+    torch.save(ck2, path)
+    m2 = load_caption_model(cfg)
+    ids2 = m2.generate_ids(torch.from_numpy(frames).to(device), [ga.bos_token_id])
+    assert torch.equal(ids2, ids)

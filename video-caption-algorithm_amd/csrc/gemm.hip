@@ -81,8 +81,9 @@ __global__ __launch_bounds__(256) void vcap_gemm_kernel(const TIn* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // split-K (gridDim.y > 1): this workgroup sums K-tiles [kt0, kt0 + nk) and adds its partial
-  // into C (f32, residual already in place) with float atomics; split 0 adds the bias
+  // split-K (gridDim.y > 1): this workgroup sums K-tiles [kt0, kt0 + nk) and stores its partial
+  // tile into slab blockIdx.y of epi.splitk_ws; vcap_splitk_reduce_kernel adds the slabs in split
+  // order (deterministic: the same sum on every run and on every stream's CU mask)
   const int nk = K / BK / (int)gridDim.y;
   const int kt0 = (int)blockIdx.y * nk;
   const bool split = gridDim.y > 1;
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(256) void vcap_gemm_kernel(const TIn* __restrict__ 
     if (nb >= N) continue;
     float bias[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bias[e] = (epi.bias && nb + e < N && (!split || blockIdx.y == 0)) ? epi.bias[nb + e] : 0.f;
+    for (int e = 0; e < 4; ++e) bias[e] = (epi.bias && nb + e < N && !split) ? epi.bias[nb + e] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wm * 64 + i * 16 + fr;
@@ -138,10 +139,8 @@ __global__ __launch_bounds__(256) void vcap_gemm_kernel(const TIn* __restrict__ 
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bias[e];
-      if (split) {  // f32 C that already holds the residual (dispatcher)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (nb + e < N) atomicAdd((float*)C + orow * ldc + nb + e, v[e]);
+      if (split) {  // raw partial sums (N % 4 == 0: dispatcher)
+        *reinterpret_cast<f32x4*>(epi.splitk_ws + ((long)blockIdx.y * M + m) * N + nb) = (f32x4){v[0], v[1], v[2], v[3]};
         continue;
       }
       if constexpr (EPI == 1) {
@@ -179,31 +178,56 @@ __global__ __launch_bounds__(256) void vcap_gemm_kernel(const TIn* __restrict__ 
   }
 }
 
+// C[orow(m)][n] = (sum over splits s = 0.. of ws[s][m][n] + bias[n]) + C[orow(m)][n]: the split-K
+// partials of an in-place residual GEMM, summed in a fixed order.
+__global__ __launch_bounds__(256) void vcap_splitk_reduce_kernel(const float* __restrict__ ws, int splits, float* C,
+                                                                 long ldc, int M, int N, GemmEpi epi) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // f32x4 index
+  const int nq = N >> 2;
+  if (i >= (long)M * nq) return;
+  const int m = (int)(i / nq), n = (int)(i - (long)m * nq) * 4;
+  f32x4 v = *reinterpret_cast<const f32x4*>(ws + (long)m * N + n);
+  for (int sp = 1; sp < splits; ++sp) v += *reinterpret_cast<const f32x4*>(ws + ((long)sp * M + m) * N + n);
+  if (epi.bias) v += *reinterpret_cast<const f32x4*>(epi.bias + n);
+  const long orow = epi.G ? (long)(m / epi.G) * epi.Gs + epi.goff + (m % epi.G) : (long)m;
+  float* c = C + orow * ldc + n;
+  *reinterpret_cast<f32x4*>(c) = v + *reinterpret_cast<const f32x4*>(c);
+}
+
 template <typename TIn, typename TOut, int EPI>
 static hipError_t launch_gemm_epi(const void* A, long lda, const void* W, long ldw, void* C, long ldc, int M, int N,
                                   int K, const GemmEpi& epi, hipStream_t s) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   // Few tiles (the CLS-only last block: M = B*T rows) leave most CUs idle through a long K
   // loop: split K over several workgroups per tile when C is f32 and already holds the
-  // residual (attn-proj / fc2 in place), adding partials with float atomics (bf16 operands
-  // only: the fp32 parity mode keeps one fixed summation order).
+  // residual (attn-proj / fc2 in place) and the caller gave a partials workspace (bf16 operands
+  // only: the fp32 parity mode keeps one summation chain).  The plan depends on the shape and
+  // the DEVICE's CU count only, never on the stream's CU mask, so a CU-masked pipelined encode
+  // sums exactly like a serial one.
   int splits = 1;
   if constexpr (sizeof(TIn) == 2 && sizeof(TOut) == 4) {
     const bool in_place = epi.bias != nullptr && epi.res == (const float*)C && epi.ldr == ldc &&
-                          (EPI == 2 || (EPI == 3 && epi.res_mode == 1 && epi.act == 0));
+                          (EPI == 2 || (EPI == 3 && epi.res_mode == 1 && epi.act == 0)) && epi.splitk_ws &&
+                          (N & 3) == 0 && (ldc & 3) == 0 && ((uintptr_t)C & 15) == 0;
     const int nkt = K / (ROWB / (int)sizeof(TIn));
-    const int ncu = vcap_stream_cus(s);
-    // (the partials' float atomics, not the K loop, dominate past a few splits: keep >= 3 K-tiles
-    // per workgroup and the grid within a quarter of the CUs)
+    const int ncu = vcap_device_cus();
+    // keep >= 3 K-tiles per workgroup and the grid within a quarter of the CUs
     if (in_place && tiles * 8 <= ncu)
       for (int c = 16; c >= 2; --c)
-        if (nkt % c == 0 && nkt / c >= 3 && tiles * c * 4 <= ncu) {
+        if (nkt % c == 0 && nkt / c >= 3 && tiles * c * 4 <= ncu &&
+            (size_t)c * M * N * sizeof(float) <= epi.splitk_bytes) {
           splits = c;
           break;
         }
   }
   hipLaunchKernelGGL((vcap_gemm_kernel<TIn, TOut, EPI>), dim3(tiles, splits), dim3(256), 0, s, (const TIn*)A, lda,
                      (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, epi);
+  if (splits > 1) {
+    if (hipError_t e = hipGetLastError()) return e;
+    const long nvec = (long)M * (N / 4);
+    hipLaunchKernelGGL(vcap_splitk_reduce_kernel, dim3((unsigned)((nvec + 255) / 256)), dim3(256), 0, s,
+                       (const float*)epi.splitk_ws, splits, (float*)C, ldc, M, N, epi);
+  }
   return hipGetLastError();
 }
 
@@ -226,6 +250,12 @@ static hipError_t launch_gemm(const void* A, long lda, const void* W, long ldw, 
 
 static int g_gemm_policy = 0;  // 0 auto, 1 always the 128x128 kernel, 2 the 256x256 kernel where it applies
 void vcap_gemm_set_policy(int p) { g_gemm_policy = p; }
+
+int vcap_device_cus() {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  return ncu;
+}
 
 // CUs the stream's kernels may use (hipExtStreamGetCUMask; the encode stream of the overlapped
 // pipeline is CU-masked), so the round arithmetic below matches what the stream really gets.

@@ -7,7 +7,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <list>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -98,6 +100,8 @@ struct VitBufs {
   void* act;
   uint8_t* xn_s;   // MXFP8 scales of xn / act
   uint8_t* act_s;
+  float* splitk;   // split-K partial slabs of the CLS-tail attn-proj / fc2 (deterministic reduce)
+  size_t splitk_bytes;
 };
 
 // operand dtype of patch-embed / qkv output / attention / attn-proj: bf16 in the MXFP8 mode
@@ -117,6 +121,8 @@ VitBufs carve_vit(Carver& c, const vcap_vit_desc* d, int B, int T) {
   const size_t patches = npatch * d->kpad * ea;
   v.act = c.take(act > patches ? act : patches);
   v.xn_s = v.act_s = nullptr;
+  v.splitk_bytes = (size_t)16 * B * T * d->dim * 4;   // <= 16 splits of the [B*T, dim] CLS rows
+  v.splitk = (float*)c.take(v.splitk_bytes);
   if (d->dtype == VCAP_DT_MXFP8) {
     v.xn_s = (uint8_t*)c.take(mx_scale_bytes((int)M, d->dim));
     v.act_s = (uint8_t*)c.take(mx_scale_bytes((int)M, d->mlp));
@@ -301,12 +307,49 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
 }
 
 // ----------------------------------------------------------------------------------- graph cache
+// Instantiated decode graphs, keyed on everything a replay bakes in (descriptor, parameters,
+// buffer addresses, device).  A bounded LRU: a long-running server that hands the decoder new
+// buffer addresses cannot grow it without limit.  Each entry remembers an event recorded after
+// its latest launch, so an evicted graph is destroyed only once its last replay has finished.
 struct GraphEntry {
   hipGraphExec_t exec = nullptr;
+  hipEvent_t done = nullptr;
+  std::list<std::string>::iterator lru;
 };
 std::mutex g_graph_mu;
 std::unordered_map<std::string, GraphEntry> g_graphs;
+std::list<std::string> g_graph_lru;  // front = most recently used
 std::unordered_map<int, hipStream_t> g_capture_streams;
+
+size_t graph_cache_cap() {
+  static size_t cap = [] {
+    const char* e = std::getenv("VCAP_GRAPH_CACHE_MAX");
+    long v = e ? std::strtol(e, nullptr, 10) : 8;
+    return (size_t)(v < 1 ? 1 : v);
+  }();
+  return cap;
+}
+
+void graph_entry_destroy(GraphEntry& ge) {
+  if (ge.done) {
+    (void)hipEventSynchronize(ge.done);
+    (void)hipEventDestroy(ge.done);
+  }
+  if (ge.exec) (void)hipGraphExecDestroy(ge.exec);
+  ge.exec = nullptr;
+  ge.done = nullptr;
+}
+
+// caller holds g_graph_mu
+void graph_cache_evict_to(size_t n) {
+  while (g_graphs.size() > n && !g_graph_lru.empty()) {
+    auto it = g_graphs.find(g_graph_lru.back());
+    g_graph_lru.pop_back();
+    if (it == g_graphs.end()) continue;
+    graph_entry_destroy(it->second);
+    g_graphs.erase(it);
+  }
+}
 
 std::string graph_key(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* ids,
                       int nids, int B, const int* out_ids, const float* logits, const void* ws) {
@@ -573,7 +616,8 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
         VCAP_TRY(vcap_vit_attention_dispatch(adt, w.qkv, w.attn, BT, N, d->heads, s, last), "attention");
     }
     // MXFP8: the attention output arrives as MXFP8 (its scales reuse xn_s, free until norm2)
-    GemmEpi e2{ly.proj_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, w.xn_s, ly.proj_ws, nullptr};
+    GemmEpi e2{ly.proj_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, w.xn_s, ly.proj_ws, nullptr,
+               last ? w.splitk : nullptr, w.splitk_bytes};
     {
       ProbeScope ps(last ? "vit.proj.cls" : "vit.proj", s);
       VCAP_TRY(vcap_gemm_dispatch(dt == VCAP_DT_MXFP8 ? dt : adt, VCAP_DT_F32, w.attn, D, ly.proj_w, D, w.x, D, Mt, D,
@@ -592,7 +636,8 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
       ProbeScope ps(last ? "vit.fc1.cls" : "vit.fc1", s);
       VCAP_TRY(vcap_gemm_dispatch(dt, dt, w.xn, D, ly.fc1_w, D, w.act, d->mlp, Mt, d->mlp, D, e3, s), "fc1");
     }
-    GemmEpi e4{ly.fc2_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, w.act_s, ly.fc2_ws, nullptr};
+    GemmEpi e4{ly.fc2_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, w.act_s, ly.fc2_ws, nullptr,
+               last ? w.splitk : nullptr, w.splitk_bytes};
     {
       ProbeScope ps(last ? "vit.fc2.cls" : "vit.fc2", s);
       VCAP_TRY(vcap_gemm_dispatch(dt, VCAP_DT_F32, w.act, d->mlp, ly.fc2_w, d->mlp, w.x, D, Mt, D, d->mlp, e4, s),
@@ -681,9 +726,19 @@ int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const
     hipError_t ei = hipGraphInstantiate(&ge.exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     VCAP_TRY(ei, "hipGraphInstantiate");
+    if (hipError_t ee = hipEventCreateWithFlags(&ge.done, hipEventDisableTiming)) {
+      (void)hipGraphExecDestroy(ge.exec);
+      return hip_fail(ee, "hipEventCreate");
+    }
+    graph_cache_evict_to(graph_cache_cap() - 1);
+    g_graph_lru.push_front(key);
+    ge.lru = g_graph_lru.begin();
     it = g_graphs.emplace(key, ge).first;
+  } else {
+    g_graph_lru.splice(g_graph_lru.begin(), g_graph_lru, it->second.lru);
   }
   VCAP_TRY(hipGraphLaunch(it->second.exec, s), "hipGraphLaunch");
+  VCAP_TRY(hipEventRecord(it->second.done, s), "hipEventRecord");
   return 0;
 }
 
@@ -826,11 +881,31 @@ int vcap_gpt2_reorder(const vcap_gpt2_desc* d, const int* src_rows, int rows, in
   return 0;
 }
 
+int vcap_decode_attention(int dtype, const void* q, const void* k_pool, const void* v_pool, const int* page_table,
+                          int maxp, void* out, int M, int heads, int S_new, int past, void* stream) {
+  if (!q || !k_pool || !v_pool || !out || M <= 0 || heads <= 0 || S_new <= 0 || past < 0 || maxp <= 0 ||
+      M % S_new)
+    return fail(VCAP_E_ARG, "vcap_decode_attention: bad arguments");
+  if (dtype != VCAP_DT_F32 && dtype != VCAP_DT_BF16) return fail(VCAP_E_ARG, "vcap_decode_attention: dtype");
+  if (past + S_new > 16 * maxp) return fail(VCAP_E_ARG, "vcap_decode_attention: context exceeds the page table");
+  if (!page_table && (dtype != VCAP_DT_BF16 || past + S_new > 64))
+    return fail(VCAP_E_UNSUPPORTED, "vcap_decode_attention: a NULL page table needs bf16 and context <= 64");
+  VCAP_TRY(vcap_decode_attention_dispatch(dtype, q, k_pool, v_pool, page_table, maxp, out, M, heads, S_new, past,
+                                          (hipStream_t)stream),
+           "vcap_decode_attention");
+  return 0;
+}
+
 void vcap_graph_cache_clear(void) {
   std::lock_guard<std::mutex> lk(g_graph_mu);
-  for (auto& kv : g_graphs)
-    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+  graph_cache_evict_to(0);
   g_graphs.clear();
+  g_graph_lru.clear();
+}
+
+int vcap_graph_cache_size(void) {
+  std::lock_guard<std::mutex> lk(g_graph_mu);
+  return (int)g_graphs.size();
 }
 
 }  // extern "C"

@@ -15,6 +15,10 @@ struct GemmEpi {
   const uint8_t* a_scale;
   const uint8_t* w_scale;
   uint8_t* c_scale;
+  // deterministic split-K (few-tile in-place residual GEMMs, bf16 operands): f32 partial slabs
+  // [split][M][N]; the partials are summed in split order by a second kernel.  nullptr: no split.
+  float* splitk_ws;
+  size_t splitk_bytes;
 };
 
 enum { PRO_LN = 0, PRO_DIRECT = 1 };
@@ -56,6 +60,8 @@ hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, co
 int vcap_gemm_k_align(int in_dt);
 // CUs a launch on stream s may use (its CU mask, else the device's CU count)
 int vcap_stream_cus(hipStream_t s);
+// CUs of the current device (launch plans that must not depend on a stream's CU mask)
+int vcap_device_cus();
 bool vcap_gemm256_ok(int in_dt, int out_dt, long lda, long ldw, long ldc, int M, int N, int K, const GemmEpi& epi);
 hipError_t vcap_gemm256_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
                                  long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s);

@@ -16,7 +16,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
 DT_F32, DT_BF16, DT_MXFP8 = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
@@ -91,6 +91,8 @@ SIGNATURES = {
     "vcap_gpt2_generate": (i32, [C.POINTER(GPT2Desc), C.POINTER(GenParams), vp, C.POINTER(C.c_int), i32, i32, vp,
                                  vp, vp, sz, vp]),
     "vcap_graph_cache_clear": (None, []),
+    "vcap_graph_cache_size": (i32, []),
+    "vcap_decode_attention": (i32, [i32, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, vp]),
     "vcap_gpt2_beam_workspace_bytes": (sz, [C.POINTER(GPT2Desc), i32, i32, i32]),
     "vcap_gpt2_prefill": (i32, [C.POINTER(GPT2Desc), vp, C.POINTER(C.c_int), i32, i32, i32, i32, vp, vp, sz, vp]),
     "vcap_gpt2_step": (i32, [C.POINTER(GPT2Desc), vp, i32, i32, i32, i32, vp, vp, sz, vp]),

@@ -18,6 +18,7 @@ num_beams > 1 -> beam search; num_beams == 1 and temperature != 1 -> sampling (t
 from __future__ import annotations
 
 import ctypes as C
+import logging
 from types import SimpleNamespace
 from typing import List, Optional, Sequence
 
@@ -29,6 +30,8 @@ from . import configs
 from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, trim_generated
 from .tokenizer import load_tokenizer
 from .weights import normalize_checkpoint, synthetic_state_dict
+
+log = logging.getLogger(__name__)
 
 
 class _Encoder:
@@ -208,16 +211,33 @@ class HipVideoCaptionModel:
 
 
 def build_state_dict(ckpt: str, vit_name: str, gpt2_name: str, weights_seed: Optional[int], prefix_len: int = 4):
-    """Reference checkpoint (model_loader.py:31-40, 74-75; weights_only load) or seeded random init."""
-    if ckpt:
-        state = torch.load(ckpt, map_location="cpu", weights_only=True)
-        sd = normalize_checkpoint(state)
-        missing = [k for k in synthetic_keys(vit_name, gpt2_name, prefix_len) if k not in sd]
-        if missing:
-            raise KeyError(f"checkpoint {ckpt} lacks {len(missing)} keys, e.g. {missing[:6]}")
-        return sd
+    """Reference checkpoint or seeded random init (core/models/model_loader.py:31-80).
+
+    Same acceptance as the reference: a raw state_dict or {"model_state": ...}, loaded with
+    strict=False - keys the checkpoint lacks keep the model's initial values (here the seeded
+    initialiser's; the reference's come from the pretrained timm / HF weights it fetches) and are
+    logged (at most 6 names), unexpected keys are logged and ignored, a shape mismatch raises as
+    load_state_dict does.  Deviation: no `weights_only=False` retry - a checkpoint that the safe
+    loader refuses is rejected rather than unpickled."""
     seed = 1 if weights_seed is None else int(weights_seed)
-    return synthetic_state_dict(seed, configs.vit_arch(vit_name), configs.gpt2_arch(gpt2_name), prefix_len)
+    init = synthetic_state_dict(seed, configs.vit_arch(vit_name), configs.gpt2_arch(gpt2_name), prefix_len)
+    if not ckpt:
+        return init
+    try:
+        state = torch.load(ckpt, map_location="cpu", weights_only=True)
+    except Exception as e:   # noqa: BLE001  (the reference logs and retries unsafely; we refuse)
+        raise RuntimeError(f"cannot load {ckpt} with torch.load(weights_only=True): {e}") from e
+    sd = normalize_checkpoint(state)
+    missing = [k for k in init if k not in sd]
+    unexpected = [k for k in sd if k not in init]
+    for k in init:
+        if k in sd and tuple(sd[k].shape) != tuple(init[k].shape):
+            raise ValueError(f"size mismatch for {k}: checkpoint {tuple(sd[k].shape)} vs model {tuple(init[k].shape)}")
+    if missing:
+        log.warning("missing keys (kept at init): %d, e.g. %s", len(missing), missing[:6])
+    if unexpected:
+        log.warning("unexpected keys (ignored): %d, e.g. %s", len(unexpected), unexpected[:6])
+    return {k: sd.get(k, v) for k, v in init.items()}
 
 
 def synthetic_keys(vit_name: str, gpt2_name: str, prefix_len: int = 4) -> List[str]:

@@ -8,7 +8,7 @@ image; the reference pins 4.57.1) as the reference reaches it fr
 text_decoder.py:131-144 with inputs_embeds (decoder_prompt_len = 0): log_softmax -> processors
 (RepetitionPenalty, NoRepeatNGram, MinLength/MinNewTokens) -> + running scores -> top-2k over
 beams x vocab -> running / finished beam updates with length_penalty=1.0, early_stopping=False
--> cache reorder.  Sampling restates `_sample` with TemperatureLogitsWarper + TopPLogitsWarper;
+-> cache reorder.  Sampling restates `_sample` with TemperatureLogitsWarper + TopKLogitsWarper(50) + TopPLogitsWarper;
 its RNG stream is torch's, so parity with the reference is distributional only.
 """
 from __future__ import annotations
@@ -66,7 +66,8 @@ def _processors(scores: torch.Tensor, seqs: torch.Tensor, rep: float, ngram: int
         match = (win[:, :, :ngram - 1] == tail[:, None, :]).all(-1)
         if bool(match.any()):
             r, w = match.nonzero(as_tuple=True)
-            scores = scores.index_put((r, win[r, w, ngram - 1]), torch.tensor(-float("inf"), device=scores.device))
+            scores = scores.index_put((r, win[r, w, ngram - 1]),
+                                      torch.tensor(-float("inf"), dtype=scores.dtype, device=scores.device))
     if L < min_new:
         scores = scores.clone()
         scores[:, eos] = -float("inf")
@@ -157,6 +158,30 @@ def beam_search(dec, prefix: torch.Tensor, prompt_ids: Sequence[int], *, num_bea
     return [list(map(int, r)) for r in best_seq[:, :out_len].cpu().tolist()]
 
 
+HF_TOP_K = 50   # GenerationConfig default; text_decoder.py:131-144 never overrides it
+
+
+def sampling_scores(logits: torch.Tensor, seqs: torch.Tensor, *, temperature: float, top_p: float, rep: float,
+                    ngram: int, min_new: int, eos: int, top_k: int = HF_TOP_K) -> torch.Tensor:
+    """The scores `_sample` draws from (HF generate with do_sample, text_decoder.py:131-144):
+    processors (RepetitionPenalty -> NoRepeatNGram -> MinNewTokens) then warpers in HF's order
+    (TemperatureLogitsWarper -> TopKLogitsWarper(50, the default the reference inherits) ->
+    TopPLogitsWarper; min_tokens_to_keep 1, filter value -inf)."""
+    sc = _processors(logits.float(), seqs, rep, ngram, min_new, eos)
+    if temperature != 1.0:
+        sc = sc / temperature
+    if top_k:
+        kth = torch.topk(sc, min(top_k, sc.shape[-1]), dim=-1).values[..., -1:]
+        sc = sc.masked_fill(sc < kth, -float("inf"))
+    if top_p < 1.0:
+        sorted_logits, sorted_idx = torch.sort(sc, descending=False)
+        cum = sorted_logits.softmax(dim=-1).cumsum(dim=-1)
+        remove = cum <= (1 - top_p)
+        remove[..., -1:] = False
+        sc = sc.masked_fill(remove.scatter(1, sorted_idx, remove), -float("inf"))
+    return sc
+
+
 @torch.no_grad()
 def sample(dec, prefix: torch.Tensor, prompt_ids: Sequence[int], *, temperature: float, top_p: float,
            max_new_tokens: int, min_new_tokens: int = 8, no_repeat_ngram_size: int = 3,
@@ -169,15 +194,8 @@ def sample(dec, prefix: torch.Tensor, prompt_ids: Sequence[int], *, temperature:
     seqs = torch.zeros(B, 0, dtype=torch.long, device=dev)
     unfinished = torch.ones(B, dtype=torch.bool, device=dev)
     for cur in range(max_new_tokens):
-        sc = _processors(logits.float(), seqs, repetition_penalty, no_repeat_ngram_size, min_new_tokens, eos)
-        if temperature != 1.0:
-            sc = sc / temperature
-        if top_p < 1.0:
-            sorted_logits, sorted_idx = torch.sort(sc, descending=False)
-            cum = sorted_logits.softmax(dim=-1).cumsum(dim=-1)
-            remove = cum <= (1 - top_p)
-            remove[..., -1:] = False
-            sc = sc.masked_fill(remove.scatter(1, sorted_idx, remove), -float("inf"))
+        sc = sampling_scores(logits, seqs, temperature=temperature, top_p=top_p, rep=repetition_penalty,
+                             ngram=no_repeat_ngram_size, min_new=min_new_tokens, eos=eos)
         nxt = torch.multinomial(F.softmax(sc, dim=-1), num_samples=1, generator=gen).squeeze(1)
         nxt = torch.where(unfinished, nxt, torch.full_like(nxt, eos))
         seqs = torch.cat([seqs, nxt[:, None]], dim=1)

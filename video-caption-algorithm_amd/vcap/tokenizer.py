@@ -22,9 +22,11 @@ class IdTokenizer:
         self.eos_token = self.pad_token = "<|endoftext|>"
 
     def encode_prompt(self, prompt: str) -> List[int]:
-        p = (prompt or "").strip()
-        if not p:
+        """text_decoder.py:119-122: an empty prompt is [BOS]; any other string (whitespace
+        included) is tokenized as given."""
+        if not prompt:
             return [self.bos_token_id]
+        p = prompt.strip()
         if p.startswith("ids:"):
             return [int(t) for t in p[4:].split()]
         raise ValueError("no GPT-2 vocab available offline: pass tokenizer_dir=<dir with vocab.json, merges.txt> "
@@ -57,12 +59,13 @@ class BPETokenizer:
         self.eos_token = self.pad_token = self.tok.eos_token
 
     def encode_prompt(self, prompt: str) -> List[int]:
-        p = (prompt or "").strip()
-        if not p:
+        """text_decoder.py:119-122: [BOS] for an empty prompt, else the unmodified string's BPE ids
+        (leading / trailing whitespace is tokenized, as the reference does)."""
+        if not prompt:
             return [self.bos_token_id]
-        if p.startswith("ids:"):
-            return [int(t) for t in p[4:].split()]
-        return list(self.tok(p).input_ids)
+        if prompt.strip().startswith("ids:"):
+            return [int(t) for t in prompt.strip()[4:].split()]
+        return list(self.tok(prompt).input_ids)
 
     def __call__(self, prompt: str, return_tensors: str = "pt"):
         return SimpleNamespace(input_ids=torch.tensor([self.encode_prompt(prompt)], dtype=torch.long))

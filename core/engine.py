@@ -101,6 +101,25 @@ class InferenceEngine:
             out.append(InferenceResult(candidates=CaptionCandidates(s1=a, s2=b, s3=d), best_key=key, best_text=text))
         return out
 
+    def load_video(self, frames_dir: str) -> torch.Tensor:
+        """frames_dir -> [1, T, 3, H, W] on the engine's device (core/preprocessing/frame_loader.py)."""
+        return load_video_tensor(frames_dir, num_frames=self.config.num_frames, image_size=self.config.image_size,
+                                 device=self.device)
+
+    def max_batch_videos(self) -> int:
+        """Videos one infer_videos call can decode: every candidate's prefill takes
+        B * (prefix_len + prompt_len) <= 128 decoder rows and a beam candidate B * num_beams <= 128
+        rows (vcap_gpt2_generate / vcap_gpt2_prefill limits)."""
+        c, tok = self.config, self.model.decoder.tokenizer
+        rows = 128
+        for prompt, preset in ((c.prompt1, c.preset1), (c.prompt2, c.preset2), (c.prompt3, c.preset3)):
+            try:
+                s0 = c.prefix_len + len(tok.encode_prompt(prompt or ""))
+            except ValueError:
+                s0 = c.prefix_len + 1   # an untokenizable prompt fails per request anyway
+            rows = min(rows, 128 // s0, 128 // max(1, preset_to_kwargs(preset).get("num_beams", 1)))
+        return max(1, rows)
+
     @torch.no_grad()
     def infer_batch(self, frames_dirs: Sequence[str]) -> List[InferenceResult]:
         """infer() for several frames directories in one engine call (each video's frames share a

@@ -10,6 +10,13 @@ one InferenceEngine.infer_batch call: one fused encode for all videos and one ba
 caption candidate, so the GPU sees batch-8 work instead of eight batch-1 calls.  Results and
 errors come back per request through futures; the registry and the GPU gate keep the reference's
 semantics.
+
+A request must fail alone, as it would in the reference's one-request-per-call service: videos
+are loaded per request (a bad frames_dir fails only its own request), grouped by shape (frame
+count and size: torch.cat of different clips would fail the whole call), cut into chunks the
+decoder takes in one call (engine.max_batch_videos(): B * (prefix + prompt) <= 128 decode rows),
+and a chunk whose engine call fails is retried one request at a time so only the offending
+request gets the error.
 """
 from __future__ import annotations
 
@@ -153,17 +160,50 @@ class BatchingInferenceService:
             self._execute(first[1], batch)
 
     def _execute(self, config, batch: List[_Item]) -> None:
-        futs = [b[3] for b in batch]
         try:
             engine = self.registry.get_engine(config)
+        except BaseException as e:  # noqa: BLE001  (no engine: every request of this config fails)
+            for b in batch:
+                b[3].set_exception(e)
+            return
+        if not hasattr(engine, "load_video"):
+            self._call(lambda items: engine.infer_batch([b[2] for b in items]), batch)
+            return
+        groups: Dict[tuple, List[Tuple[_Item, object]]] = {}
+        for b in batch:
+            try:
+                with self.gate.acquire():
+                    v = engine.load_video(b[2])
+            except BaseException as e:  # noqa: BLE001
+                b[3].set_exception(e)
+                continue
+            groups.setdefault(tuple(v.shape[1:]), []).append((b, v))
+        cap = max(1, min(self.max_batch, int(engine.max_batch_videos())))
+        for members in groups.values():
+            for i in range(0, len(members), cap):
+                chunk = members[i:i + cap]
+                vids = {id(b): v for b, v in chunk}
+
+                def run(items, vids=vids):
+                    import torch
+                    return engine.infer_videos(torch.cat([vids[id(b)] for b in items], dim=0))
+                self._call(run, [b for b, _ in chunk])
+
+    def _call(self, fn, items: List[_Item]) -> None:
+        """One engine call for `items`; on failure retry each request alone (only the request that
+        fails on its own gets the error)."""
+        try:
             with self.gate.acquire():
-                results = engine.infer_batch([b[2] for b in batch])
-            if len(results) != len(batch):
-                raise RuntimeError(f"engine returned {len(results)} results for {len(batch)} requests")
-            self.batches.append(len(batch))
-            for f, r in zip(futs, results):
-                f.set_result(r)
-        except BaseException as e:  # every request of the failed call gets the error
-            for f in futs:
-                if not f.done():
-                    f.set_exception(e)
+                results = fn(items)
+            if len(results) != len(items):
+                raise RuntimeError(f"engine returned {len(results)} results for {len(items)} requests")
+        except BaseException as e:  # noqa: BLE001
+            if len(items) == 1:
+                items[0][3].set_exception(e)
+            else:
+                for it in items:
+                    self._call(fn, [it])
+            return
+        self.batches.append(len(items))
+        for it, r in zip(items, results):
+            it[3].set_result(r)

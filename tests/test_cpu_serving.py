@@ -1,6 +1,7 @@
 """Serving batcher (core/serving.py) on a fake engine: requests coalesce into engine calls of at
 most max_batch per engine key, results route back to their request, errors reach every request
-of the failed call, validation mirrors server/services/inference_service.py:50-55."""
+of the failed call are retried alone (only the offending request fails), videos of different
+shapes never share a call, validation mirrors server/services/inference_service.py:50-55."""
 import threading
 from dataclasses import replace
 
@@ -91,3 +92,60 @@ def test_validation_matches_reference_service(tmp_path):
     svc.close()
     with pytest.raises(RuntimeError):
         svc.submit(d, InferenceConfig())
+
+
+class FakeVideoEngine:
+    """load_video / infer_videos protocol: frames_dir names encode the clip shape ("t4" = 4 frames)."""
+
+    def __init__(self, config):
+        self.config = config
+        self.calls = []
+
+    def load_video(self, d):
+        import torch
+        if d.endswith("unreadable"):
+            raise FileNotFoundError("no frames")
+        t = int(d.rsplit("t", 1)[1].split("_")[0])
+        v = torch.zeros(1, t, 3, 4, 4)
+        v[0, 0, 0, 0, 0] = float(d.rsplit("_", 1)[1])
+        return v
+
+    def max_batch_videos(self):
+        return 3
+
+    def infer_videos(self, videos):
+        self.calls.append(tuple(videos.shape))
+        ids = [int(x) for x in videos[:, 0, 0, 0, 0].tolist()]
+        if 13 in ids:
+            raise RuntimeError("bad video 13")
+        return [f"T{videos.shape[1]}:{i}" for i in ids]
+
+
+def test_video_batches_group_by_shape_cap_and_isolate_errors(tmp_path):
+    eng = {}
+
+    def factory(cfg):
+        eng["e"] = FakeVideoEngine(cfg)
+        return eng["e"]
+
+    svc = BatchingInferenceService(ModelRegistry(factory), max_batch=8, max_wait_ms=300)
+    cfg = InferenceConfig(weights_seed=1)
+    names = [f"t4_{i}" for i in range(5)] + [f"t8_{i}" for i in range(10, 15)] + ["t4_unreadable"]
+    dirs = []
+    for n in names:
+        (tmp_path / n).mkdir()
+        dirs.append(str(tmp_path / n))
+    futs = [svc.submit(d, cfg) for d in dirs]
+    out = []
+    for f in futs:
+        try:
+            out.append(f.result(timeout=30))
+        except Exception as e:  # noqa: BLE001
+            out.append(type(e).__name__)
+    svc.close()
+    assert out[:5] == [f"T4:{i}" for i in range(5)]
+    assert out[5:10] == ["T8:10", "T8:11", "T8:12", "RuntimeError", "T8:14"]
+    assert out[10] == "FileNotFoundError"
+    shapes = eng["e"].calls
+    assert all(s[0] <= 3 for s in shapes)               # engine.max_batch_videos cap
+    assert {s[1] for s in shapes} == {4, 8}             # never mixed in one call

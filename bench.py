@@ -61,7 +61,9 @@ def parse():
     ap.add_argument("--decode-blocks", type=int, default=128,
                     help="cap the decode GEMV grids near this many workgroups (0 = whole-chip grids)")
     ap.add_argument("--dec-lanes", type=int, default=2,
-                    help="decodes in flight at once (each batch still decoded alone, own stream + graph)")
+                    help="decodes in flight at once (own stream + workspace + graph each)")
+    ap.add_argument("--dec-group", type=int, default=1,
+                    help="consecutive batches decoded together as one decode of group*batch rows")
     ap.add_argument("--confine-decode", action="store_true",
                     help="mask the decode streams to the reserved CUs (default: unmasked, high priority)")
     ap.add_argument("--gemm-policy", type=int, default=0, help="vcap_set_gemm_policy value for A/B runs (0 = auto)")
@@ -225,18 +227,23 @@ def main():
     else:
         cfg = GenConfig.raw_greedy(args.max_new, ga.eos_token_id, not args.no_graph)
     cfg.max_blocks = 0 if args.serial else args.decode_blocks
-    # every batch's ids -> row `slot_of[0]` of a per-run buffer, on the batch's own decode lane
+    # every timed batch's ids -> row (submission index - timed_base) of a per-run buffer, copied on
+    # the decode lane that produced them
     ids_all = torch.zeros(max(args.steps, 1), B, args.max_new, dtype=torch.int32, device=dev)
-    slot_of = [0]
+    timed_base = [1 << 30]
 
-    def keep(ids):
-        ids_all[slot_of[0]].copy_(ids)
+    def keep(ids, first_k):
+        for i in range(ids.shape[0] // B):
+            t = first_k + i - timed_base[0]
+            if 0 <= t < args.steps:
+                ids_all[t].copy_(ids[i * B:(i + 1) * B])
         return ids
 
     pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev, gather=keep if world > 1 else None,
                            reserve_cus=0 if args.serial else args.reserve_cus,
                            dec_lanes=1 if args.serial else args.dec_lanes,
-                           confine_decode=args.confine_decode and not args.serial)
+                           confine_decode=args.confine_decode and not args.serial,
+                           dec_group=1 if args.serial else args.dec_group)
 
     def step(t0=None, t1=None, t2=None):
         pipe.submit(video, t0, t1, t2)
@@ -245,7 +252,7 @@ def main():
 
     for _ in range(max(args.warmup, 1)):
         step()
-    pipe.synchronize()
+    pipe.synchronize()   # (flushes a partial decode group)
     torch.cuda.synchronize(dev)
     if world > 1:
         gather_ids(ids_all, world)  # communicator set-up outside the timed region
@@ -261,11 +268,11 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    timed_base[0] = pipe.k
     t0 = time.perf_counter()
     for k in range(args.steps):
-        slot_of[0] = k
         step(starts[k], mids[k], ends[k])
-    pipe.synchronize()
+    pipe.synchronize()   # decodes a trailing partial group too
     if world > 1:
         gathered = gather_ids(ids_all, world)  # [world * steps, B, max_new] on every rank
     torch.cuda.synchronize(dev)
@@ -286,7 +293,6 @@ def main():
             # the pipeline's external CU-masked stream that close() destroys); the encode waits on it
             vid_h.copy_(pinned, non_blocking=True)
             pipe.s_enc.wait_stream(torch.cuda.current_stream(dev))
-            slot_of[0] = 0
             ids_dev = pipe.result(pipe.submit(vid_h))
             ids_host = (gather_ids(ids_dev, world) if world > 1 else ids_dev).cpu()
             host_lat.append(time.perf_counter() - t_h)
@@ -295,7 +301,7 @@ def main():
         del ids_host, pinned, vid_h
 
     # caption lengths of the last timed batch (new tokens up to and including EOS)
-    last = pipe.result((pipe.k - 1) % pipe.depth).cpu()
+    last = pipe.result(pipe.last_slot).cpu()
     # parity of what was timed (outside the timed region): the last batch's ids against the fp32
     # parity mode (token-exact against the reference: tests/test_gpu_parity.py) on the same frames
     parity = None
@@ -368,13 +374,13 @@ def main():
                        "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}",
                        "decode_block_cap": cfg.max_blocks,
                        "schedule": "serial" if args.serial else
-                       f"encode(k+1) overlapped with decode(k) on 2 HIP streams (encode CU-masked off "
-                       f"{args.reserve_cus} CUs)" if args.dec_lanes == 1 else
-                       f"encode(k+{args.dec_lanes}) overlapped with {args.dec_lanes} decodes in flight "
-                       f"(batches k..k+{args.dec_lanes - 1}, one HIP stream + graph each; encode CU-masked off "
-                       f"{args.reserve_cus} CUs)"},
+                       f"CU-masked encode stream (off {args.reserve_cus} CUs) overlapped with {args.dec_lanes} decode "
+                       f"lane(s) in flight; each decode = {args.dec_group} consecutive batch(es) as one "
+                       f"{args.dec_group * B}-row greedy decode graph",
+                       "dec_lanes": 1 if args.serial else args.dec_lanes,
+                       "dec_group": 1 if args.serial else args.dec_group},
             "value_definition": "pipelined throughput: videos captioned / wall time of the timed steps "
-                                "(encode of batch k+2 overlapped with the decodes of batches k, k+1)",
+                                "(encodes overlapped with the decodes of earlier batches)",
             "captions_per_s_b_over_p50": world * B / (p50 / 1e3),
             "p50_latency_ms": p50,
             "new_tokens_per_caption": {"mean": sum(lens) / len(lens), "max": max(lens),

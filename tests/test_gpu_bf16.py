@@ -143,10 +143,12 @@ def test_lm_head_processor_epilogue_every_step(device, prec):
         fin |= ids64[:, s] == eos
 
 
-def test_bf16_pipeline_bit_identical_to_serial(device):
-    """The bench schedule (vcap/pipeline.py: CU-masked encode stream, two decode lanes with capped
-    grids, own workspaces / graphs) gives bit-identical bf16 encodes and ids to a serial bf16
-    encode + generate_ids on the default stream (deterministic split-K, mask-independent plans)."""
+@pytest.mark.parametrize("lanes,group", [(2, 1), (1, 2), (2, 2)])
+def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group):
+    """The bench schedule (vcap/pipeline.py: CU-masked encode stream, decode lanes with capped
+    grids, own workspaces / graphs, optionally `group` batches decoded as one decode of group*8
+    rows) gives bit-identical bf16 encodes and ids to a serial bf16 encode + generate_ids on the
+    default stream (deterministic split-K, mask-independent plans, row-independent decode)."""
     from vcap.pipeline import CaptionPipeline
     meta, g, va, ga, sd, frames, enc, pre, dec = _models("bf16", device)
     video = torch.from_numpy(frames).to(device)
@@ -154,9 +156,10 @@ def test_bf16_pipeline_bit_identical_to_serial(device):
     ids_serial = dec.generate_ids(pre_serial, [ga.bos_token_id], _hf_cfg(ga)).clone()
     cfg = _hf_cfg(ga, max_blocks=128)
     pipe = CaptionPipeline(enc, pre, dec, cfg, video.shape[0], [ga.bos_token_id], device, reserve_cus=32,
-                           dec_lanes=2)
+                           dec_lanes=lanes, dec_group=group)
     try:
         slots = [pipe.submit(video) for _ in range(5)]
+        pipe.synchronize()
         for slot in slots[-3:]:
             assert torch.equal(pipe.result(slot), ids_serial)
             assert torch.equal(pipe.prefix_bufs[slot], pre_serial)

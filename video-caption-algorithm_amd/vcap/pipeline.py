@@ -7,10 +7,17 @@ time per batch approaches max(encode, decode) instead of their sum.  Every batch
 full encode + prefix + decode; double-buffered prefix/ids buffers and events keep batch k+2's
 encode from overwriting buffers batch k's decode still reads.
 
-`dec_lanes` > 1 keeps that many decodes in flight at once (batch k on lane k % dec_lanes, each
-lane its own stream, KV/scratch workspace and captured graph).  A decode is a chain of ~60
+`dec_lanes` > 1 keeps that many decodes in flight at once (decode group g on lane g % dec_lanes,
+each lane its own stream, KV/scratch workspace and captured graph).  A decode is a chain of ~60
 dependent launches per token that occupies a fraction of the CUs it is given, so a second
-independent chain fills the gaps of the first; each batch is still decoded on its own (B rows).
+independent chain fills the gaps of the first.
+
+`dec_group` > 1 decodes that many consecutive encode batches together as one decode of
+dec_group * B rows: the decode step is latency-bound, so 16 rows cost ~8 % more than 8 rows per
+token step (every step streams the 247 MB of weights once instead of once per batch).  Rows are
+independent in every decode kernel (per-row MFMA outputs, per-row processors), so a batch's ids
+are bit-identical whichever group it is decoded in (tests/test_gpu_bf16.py).  The price is latency:
+a batch waits for the next batch's encode before its decode starts.
 """
 from __future__ import annotations
 
@@ -27,13 +34,15 @@ from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, _Workspa
 class CaptionPipeline:
     def __init__(self, encoder: HipViTEncoder, prefix: HipPrefix, decoder: HipGPT2Decoder, cfg: GenConfig,
                  batch: int, prompt_ids: Sequence[int], device, depth: int = 2, gather=None,
-                 reserve_cus: int = 0, dec_lanes: int = 1, confine_decode: bool = False):
+                 reserve_cus: int = 0, dec_lanes: int = 1, confine_decode: bool = False, dec_group: int = 1):
         self.enc, self.pre, self.dec, self.cfg = encoder, prefix, decoder, cfg
         self.prompt_ids = list(prompt_ids)
         self.device = torch.device(device)
-        if dec_lanes < 1:
-            raise ValueError("dec_lanes must be >= 1")
+        if dec_lanes < 1 or dec_group < 1:
+            raise ValueError("dec_lanes and dec_group must be >= 1")
         self.lanes = int(dec_lanes)
+        self.group = int(dec_group)
+        self.batch = int(batch)
         depth = max(int(depth), self.lanes + 1)   # one slot being encoded + one per decoding lane
         self.depth = depth
         # The decode chain is latency-bound: give its stream the higher priority so its small
@@ -67,50 +76,86 @@ class CaptionPipeline:
         self.s_dec = self.s_decs[0]
         self.dec_ws = [decoder.ws] + [_Workspace(self.device) for _ in range(self.lanes - 1)]
         E = decoder.arch.n_embd
-        self.prefix_bufs = [torch.empty(batch, prefix.prefix_len, E, device=self.device) for _ in range(depth)]
-        self.ids_bufs = [torch.empty(batch, cfg.max_new_tokens, dtype=torch.int32, device=self.device)
-                         for _ in range(depth)]
+        G = self.group
+        # slot = one decode group: G consecutive batches' prefixes side by side, decoded as G*B rows
+        self.group_prefix = [torch.empty(G * batch, prefix.prefix_len, E, device=self.device) for _ in range(depth)]
+        self.group_ids = [torch.empty(G * batch, cfg.max_new_tokens, dtype=torch.int32, device=self.device)
+                          for _ in range(depth)]
         self.enc_done = [torch.cuda.Event() for _ in range(depth)]
         self.dec_done: List[Optional[torch.cuda.Event]] = [None] * depth
-        self.gather = gather          # optional callable(ids) -> gathered ids, run on the decode stream
-        self.outputs: List[Optional[torch.Tensor]] = [None] * depth
+        self.gather = gather          # optional callable(ids, first_k) -> ids, run on the decode stream
+        self.outputs: List[Optional[torch.Tensor]] = [None] * (depth * G)
+        self._pending_end: List[torch.cuda.Event] = []
         self.k = 0
+
+    @property
+    def prefix_bufs(self) -> List[torch.Tensor]:
+        """Per-submission-slot prefix views (slot = k % (depth * dec_group))."""
+        B = self.batch
+        return [gp[j * B:(j + 1) * B] for gp in self.group_prefix for j in range(self.group)]
 
     def submit(self, video: torch.Tensor, t_start: Optional[torch.cuda.Event] = None,
                t_mid: Optional[torch.cuda.Event] = None, t_end: Optional[torch.cuda.Event] = None) -> int:
-        slot = self.k % self.depth
+        """Encode one batch; launch the decode of its group once the group's last batch is encoded.
+        Returns the submission slot for result() (k % (depth * dec_group)).  With dec_group > 1,
+        t_end of a batch is recorded after its GROUP's decode; `gather(ids, first_k)` receives the
+        group's [G*B, L] ids and the submission index of its first batch."""
+        G, B = self.group, self.batch
+        g, j = divmod(self.k, G)
+        slot = g % self.depth
         with torch.cuda.stream(self.s_enc):
-            if self.dec_done[slot] is not None:
-                self.s_enc.wait_event(self.dec_done[slot])   # buffers of batch k-depth are free
+            if j == 0 and self.dec_done[slot] is not None:
+                self.s_enc.wait_event(self.dec_done[slot])   # buffers of group g-depth are free
             if t_start is not None:
                 t_start.record()
-            self.enc.encode(video, self.pre, out_prefix=self.prefix_bufs[slot])
+            self.enc.encode(video, self.pre, out_prefix=self.group_prefix[slot][j * B:(j + 1) * B])
             if t_mid is not None:
                 t_mid.record()
             self.enc_done[slot].record()
-        lane = self.k % self.lanes
+        if t_end is not None:
+            self._pending_end.append(t_end)
+        self.k += 1
+        self.last_slot = slot * G + j
+        if j == G - 1:
+            self._decode_group(g)
+        return self.last_slot
+
+    def flush(self) -> None:
+        """Decode a partially filled group now (its unfilled rows hold stale prefixes; their ids
+        are ignored).  Called before waiting on results when k is not a multiple of dec_group."""
+        if self.k % self.group:
+            g = self.k // self.group
+            self.k = (g + 1) * self.group
+            self._decode_group(g)
+
+    def _decode_group(self, g: int) -> None:
+        G, B = self.group, self.batch
+        slot, lane = g % self.depth, g % self.lanes
         s_dec = self.s_decs[lane]
         with torch.cuda.stream(s_dec):
             s_dec.wait_event(self.enc_done[slot])
-            self.dec.generate_ids(self.prefix_bufs[slot], self.prompt_ids, self.cfg, out=self.ids_bufs[slot],
+            self.dec.generate_ids(self.group_prefix[slot], self.prompt_ids, self.cfg, out=self.group_ids[slot],
                                   workspace=self.dec_ws[lane])
-            out = self.ids_bufs[slot]
+            out = self.group_ids[slot]
             if self.gather is not None:
-                out = self.gather(out)
-            self.outputs[slot] = out
-            if t_end is not None:
-                t_end.record()
+                out = self.gather(out, g * G)
+            for i in range(G):
+                self.outputs[slot * G + i] = out[i * B:(i + 1) * B]
+            for ev in self._pending_end:
+                ev.record()
+            self._pending_end = []
             ev = torch.cuda.Event()
             ev.record()
             self.dec_done[slot] = ev
-        self.k += 1
-        return slot
 
     def result(self, slot: int) -> torch.Tensor:
-        self.dec_done[slot].synchronize()
+        if self.k % self.group and slot // self.group == (self.k // self.group) % self.depth:
+            self.flush()   # the slot's group has not been decoded yet
+        self.dec_done[slot // self.group].synchronize()
         return self.outputs[slot]
 
     def synchronize(self) -> None:
+        self.flush()
         self.s_enc.synchronize()
         for s in self.s_decs:
             s.synchronize()

@@ -108,16 +108,17 @@ class InferenceEngine:
 
     def max_batch_videos(self) -> int:
         """Videos one infer_videos call can decode: every candidate's prefill takes
-        B * (prefix_len + prompt_len) <= 128 decoder rows and a beam candidate B * num_beams <= 128
-        rows (vcap_gpt2_generate / vcap_gpt2_prefill limits)."""
+        B * (prefix_len + prompt_len) decoder rows and a beam candidate B * num_beams rows, both
+        within vcap_gpt2_max_rows()."""
+        from vcap import _native as N
         c, tok = self.config, self.model.decoder.tokenizer
-        rows = 128
+        rows = limit = int(N.lib().vcap_gpt2_max_rows())
         for prompt, preset in ((c.prompt1, c.preset1), (c.prompt2, c.preset2), (c.prompt3, c.preset3)):
             try:
                 s0 = c.prefix_len + len(tok.encode_prompt(prompt or ""))
             except ValueError:
                 s0 = c.prefix_len + 1   # an untokenizable prompt fails per request anyway
-            rows = min(rows, 128 // s0, 128 // max(1, preset_to_kwargs(preset).get("num_beams", 1)))
+            rows = min(rows, limit // s0, limit // max(1, preset_to_kwargs(preset).get("num_beams", 1)))
         return max(1, rows)
 
     @torch.no_grad()

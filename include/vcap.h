@@ -199,6 +199,8 @@ int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const
 void vcap_graph_cache_clear(void);
 /* number of instantiated decode graphs held by the cache (bounded LRU, VCAP_GRAPH_CACHE_MAX) */
 int vcap_graph_cache_size(void);
+/* decoder rows one call may carry: B * (prefix + prompt) at the prefill, B * num_beams per step */
+int vcap_gpt2_max_rows(void);
 
 /* ---- causal decode attention over the paged KV cache (one GPT-2 layer; HF GPT2Attention's
  *      sdpa path at decode time, text_decoder.py:131-144 -> modeling_gpt2): q [M, H*64] (M = seqs *
@@ -207,6 +209,29 @@ int vcap_graph_cache_size(void);
  *      to positions 0 .. past + (m % S_new) of its sequence. ---- */
 int vcap_decode_attention(int dtype, const void* q, const void* k_pool, const void* v_pool, const int* page_table,
                           int maxp, void* out, int M, int heads, int S_new, int past, void* stream);
+
+/* ---- device beam search (HF `_beam_search` as text_decoder.py:131-144 reaches it for the
+ *      `precise` / `detailed` presets: log_softmax -> RepetitionPenalty -> NoRepeatNGram ->
+ *      MinNewTokens -> + beam scores -> top-2*num_beams, length_penalty, early_stopping=False).
+ *      The whole search (prefill + max_new steps + bookkeeping) is one call, replayed as one
+ *      hipGraph; out_ids [B, max_new] = each sequence's best finished hypothesis (EOS-padded),
+ *      out_len [B] = its generated length (HF returns the first max(out_len) columns). ---- */
+typedef struct vcap_beam_params {
+  int num_beams;
+  int max_new_tokens;
+  int min_new_tokens;
+  int no_repeat_ngram_size;
+  float repetition_penalty;
+  float length_penalty;
+  int early_stopping;  /* only 0 (False) */
+  int eos_token_id;
+  int use_graph;
+} vcap_beam_params;
+size_t vcap_gpt2_beam_search_workspace_bytes(const vcap_gpt2_desc* d, int B, int num_beams, int S0,
+                                             int max_new_tokens);
+int vcap_gpt2_beam_search(const vcap_gpt2_desc* d, const vcap_beam_params* bp, const float* prefix,
+                          const int* prompt_ids, int prompt_len, int B, int* out_ids, int* out_len, void* workspace,
+                          size_t ws_bytes, void* stream);
 
 /* ---- step-wise decode for host-driven search (beam search / sampling).  One state carved for
  *      `rows` decoder rows lives in the caller's workspace across calls:

@@ -143,7 +143,7 @@ def test_lm_head_processor_epilogue_every_step(device, prec):
         fin |= ids64[:, s] == eos
 
 
-@pytest.mark.parametrize("lanes,group", [(2, 1), (1, 2), (2, 2)])
+@pytest.mark.parametrize("lanes,group", [(2, 1), (1, 2), (2, 2), (1, 4)])
 def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group):
     """The bench schedule (vcap/pipeline.py: CU-masked encode stream, decode lanes with capped
     grids, own workspaces / graphs, optionally `group` batches decoded as one decode of group*8

@@ -53,12 +53,15 @@ def test_medium_greedy_fp32_token_identical_and_logits(device):
     assert again == got
 
 
-def test_medium_beam4_fp32_matches_reference(device):
-    """preset "detailed" (core/inference.py:10): num_beams 4, max_new_tokens 40."""
+@pytest.mark.parametrize("impl", ["device", "host"])
+def test_medium_beam4_fp32_matches_reference(device, impl):
+    """preset "detailed" (core/inference.py:10): num_beams 4, max_new_tokens 40 - the device search
+    (one hipGraph) and the host-bookkeeping restatement."""
     meta, g, va, ga, enc, pre, dec, video = _models(device)
     prefix = torch.from_numpy(g["inputs_embeds"][:, :4].copy()).to(device)
-    rows = search.beam_search(dec, prefix, meta["prompt_ids"], num_beams=4, max_new_tokens=40, min_new_tokens=8,
-                              no_repeat_ngram_size=3, repetition_penalty=1.1, eos=ga.eos_token_id)
+    fn = search.beam_search_device if impl == "device" else search.beam_search
+    rows = fn(dec, prefix, meta["prompt_ids"], num_beams=4, max_new_tokens=40, min_new_tokens=8,
+              no_repeat_ngram_size=3, repetition_penalty=1.1, eos=ga.eos_token_id)
     exp = g["beam4_ids"]
     assert np.array_equal(np.array(rows, dtype=np.int32), exp), (rows, exp)
 

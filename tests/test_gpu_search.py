@@ -24,10 +24,17 @@ def _prefix(name, device):
 
 @pytest.mark.parametrize("name,nb,mx", [("tiny", 3, 24), ("tiny", 4, 40), ("tiny_prompt", 3, 24),
                                         ("b16_b2", 3, 24), ("b16_b2", 4, 40)])
-def test_beam_search_fp32_matches_reference(device, name, nb, mx):
+@pytest.mark.parametrize("impl", ["device", "device_eager", "host"])
+def test_beam_search_fp32_matches_reference(device, name, nb, mx, impl):
+    """Beam ids equal the reference's HF beam search: the device search (csrc/beam.hip, replayed
+    graph and eager launches) and the host-bookkeeping restatement."""
     meta, g, ga, dec, pre = _prefix(name, device)
-    rows = search.beam_search(dec, pre, meta["prompt_ids"], num_beams=nb, max_new_tokens=mx, min_new_tokens=8,
-                              no_repeat_ngram_size=3, repetition_penalty=1.1, eos=ga.eos_token_id)
+    kw = dict(num_beams=nb, max_new_tokens=mx, min_new_tokens=8, no_repeat_ngram_size=3, repetition_penalty=1.1,
+              eos=ga.eos_token_id)
+    if impl == "host":
+        rows = search.beam_search(dec, pre, meta["prompt_ids"], **kw)
+    else:
+        rows = search.beam_search_device(dec, pre, meta["prompt_ids"], use_graph=impl == "device", **kw)
     exp = g[f"beam{nb}_ids"]
     assert np.array_equal(np.array(rows, dtype=np.int32), exp), (rows, exp)
 

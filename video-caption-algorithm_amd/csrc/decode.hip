@@ -42,6 +42,9 @@ __global__ __launch_bounds__(256) void vcap_rows_pack_kernel(const T* __restrict
 }
 
 VCAP_DEV const u32x4* packed_frag(const void* w, int tile, int nslab, int slab, int lane) {
+#ifdef VCAP_DIAG_W0   // diagnostic build only: every workgroup reads tile 0's weights (L2-resident)
+  tile = 0;
+#endif
   return reinterpret_cast<const u32x4*>(w) + ((long)tile * nslab + slab) * 64 + lane;
 }
 
@@ -84,6 +87,11 @@ VCAP_DEV void rows_epilogue(const RowsGemmArgs& a, int m0, const float (*red)[MT
       if (ok) ((T*)a.out)[(long)m * a.ldo + n] = Num<T>::from_f(gelu_tanh(v));
     } else if constexpr (EPI == EPI_STORE) {
       if (ok) ((T*)a.out)[(long)m * a.ldo + n] = Num<T>::from_f(v);
+    } else if constexpr (EPI == EPI_LSE) {
+      if (m < M) {
+        if (n < N) a.logits_raw[(long)m * N + n] = v;
+        lg[ml][j * 16 + col] = n < N ? v : -INFINITY;
+      }
     } else {  // EPI_LOGITS: RepetitionPenalty -> NoRepeatNGram -> MinNewTokens (HF processor order)
       if (m < M) {
         float sv = -INFINITY;
@@ -95,6 +103,22 @@ VCAP_DEV void rows_epilogue(const RowsGemmArgs& a, int m0, const float (*red)[MT
           if (n == a.eos && a.gen_len < a.min_new) sv = -INFINITY;
         }
         lg[ml][j * 16 + col] = sv;
+      }
+    }
+  }
+  if constexpr (EPI == EPI_LSE) {
+    // log_softmax statistics of this workgroup's columns: (max, sum exp(x - max)) per row
+    __syncthreads();
+    for (int ml = wave; ml < MT * 16 && m0 + ml < M; ml += 4) {
+      float mx = -INFINITY;
+      for (int c = lane; c < NTB * 16; c += 64) mx = fmaxf(mx, lg[ml][c]);
+      mx = wave_max(mx);
+      float sm = 0.f;
+      for (int c = lane; c < NTB * 16; c += 64) sm += expf(lg[ml][c] - mx);
+      sm = wave_sum(sm);
+      if (lane == 0) {
+        a.part_val[(long)(m0 + ml) * a.nblk + blockIdx.x] = mx;
+        a.part_sum[(long)(m0 + ml) * a.nblk + blockIdx.x] = sm;
       }
     }
   }
@@ -165,7 +189,7 @@ template <typename T, int MT, int NTB, int PRO, int EPI, int NSL>
 __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char dyn[];  // PRO_LN: A tile [MT*16][K] T
   constexpr int E = Frag<T>::kElems, KS = 4 * E, MP = MT * 16, NE = MT * NTB;
-  constexpr int LGM = EPI == EPI_LOGITS ? MP : 1;
+  constexpr int LGM = (EPI == EPI_LOGITS || EPI == EPI_LSE) ? MP : 1;
   constexpr int KC = NSL * KS * 4 / 256;  // f32x4 chunks per lane of a K-long row (PRO_LN)
   constexpr int RPW = MP / 4;             // LN rows per wave
   __shared__ __attribute__((aligned(16))) float red[4][NE * 256];
@@ -310,7 +334,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
   constexpr int U = NTB >= 4 ? 2 : 8 / NTB;  // slabs per chunk: U*NTB weight fragments in flight
   constexpr int MP = MT * 16;
   constexpr int NE = MT * NTB;
-  constexpr int LGM = EPI == EPI_LOGITS ? MP : 1;
+  constexpr int LGM = (EPI == EPI_LOGITS || EPI == EPI_LSE) ? MP : 1;
   __shared__ __attribute__((aligned(16))) float red[4][NE * 256];
   __shared__ float lg[LGM][NTB * 16];
   __shared__ unsigned char s_rep[LGM][NTB * 16], s_ban[LGM][NTB * 16];
@@ -579,9 +603,9 @@ template <typename T>
 __global__ __launch_bounds__(256) void vcap_prefill_embed_kernel(const float* __restrict__ prefix, int P,
                                                                  PromptIds prompt, const T* __restrict__ wte,
                                                                  const float* __restrict__ wpe, float* __restrict__ h,
-                                                                 int S0, int E, int pos0) {
+                                                                 int S0, int E, int pos0, int prefix_rep) {
   const int m = blockIdx.x;
-  const int s = m / S0, i = m % S0;
+  const int s = m / S0 / prefix_rep, i = m % S0;   // prefix_rep rows (beams) share sequence s's prefix
   for (int c = threadIdx.x; c < E; c += 256) {
     float v = (i < P) ? prefix[((long)s * P + i) * E + c] : Num<T>::to_f(wte[(long)prompt.ids[i - P] * E + c]);
     h[(long)m * E + c] = v + wpe[(long)(pos0 + i) * E + c];
@@ -754,7 +778,7 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
 // 16-column tiles per workgroup: the lm_head always takes 4 (argmax partials per 64 columns);
 // the projections take 1 unless a grid cap asks for wider workgroups (2 or 4 tiles).
 static int rows_ntb(int epi, int N = 0, int max_blocks = 0) {
-  if (epi == EPI_LOGITS) return 4;
+  if (epi == EPI_LOGITS || epi == EPI_LSE) return 4;
   const int tiles = (N + 15) / 16;
   if (max_blocks <= 0 || tiles <= max_blocks) return 1;
   return tiles <= 2 * max_blocks ? 2 : 4;
@@ -785,7 +809,8 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
   if (pro == PRO_LN && epi == EPI_QKV) { VCAP_ROWS_NT(TT, PRO_LN, EPI_QKV) }                \
   if (pro == PRO_LN && epi == EPI_GELU) { VCAP_ROWS_NT(TT, PRO_LN, EPI_GELU) }              \
   if (pro == PRO_DIRECT && epi == EPI_RESID) { VCAP_ROWS_NT(TT, PRO_DIRECT, EPI_RESID) }    \
-  if (pro == PRO_LN && epi == EPI_LOGITS) { VCAP_ROWS(TT, PRO_LN, EPI_LOGITS, 4) }
+  if (pro == PRO_LN && epi == EPI_LOGITS) { VCAP_ROWS(TT, PRO_LN, EPI_LOGITS, 4) }   \
+  if (pro == PRO_LN && epi == EPI_LSE) { VCAP_ROWS(TT, PRO_LN, EPI_LSE, 4) }
   if (dt == VCAP_DT_BF16) {
     VCAP_ROWS_EPI(bf16_t)
   } else {
@@ -911,7 +936,8 @@ hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc,
 }
 
 hipError_t vcap_prefill_embed_dispatch(int dt, const float* prefix, int P, const int* ids, int nids, const void* wte,
-                                       const float* wpe, float* h, int B, int E, hipStream_t s, int pos0) {
+                                       const float* wpe, float* h, int B, int E, hipStream_t s, int pos0,
+                                       int prefix_rep) {
   if (nids > 64) return hipErrorInvalidValue;
   PromptIds pr;
   pr.n = nids;
@@ -919,10 +945,10 @@ hipError_t vcap_prefill_embed_dispatch(int dt, const float* prefix, int P, const
   const int S0 = P + nids;
   if (dt == VCAP_DT_BF16)
     hipLaunchKernelGGL((vcap_prefill_embed_kernel<bf16_t>), dim3(B * S0), dim3(256), 0, s, prefix, P, pr,
-                       (const bf16_t*)wte, wpe, h, S0, E, pos0);
+                       (const bf16_t*)wte, wpe, h, S0, E, pos0, prefix_rep);
   else
     hipLaunchKernelGGL((vcap_prefill_embed_kernel<float>), dim3(B * S0), dim3(256), 0, s, prefix, P, pr,
-                       (const float*)wte, wpe, h, S0, E, pos0);
+                       (const float*)wte, wpe, h, S0, E, pos0, prefix_rep);
   return hipGetLastError();
 }
 

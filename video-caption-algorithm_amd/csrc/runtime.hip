@@ -57,6 +57,10 @@ struct Carver {
 
 bool attn_lds_configured = false;
 
+// Decoder rows one call may carry (B * (prefix + prompt) at the prefill, rows of a step).  Rows go
+// through the GEMV kernels in 16 / 32-row chunks (blockIdx.y), so this bounds workspace sizes only.
+constexpr int kMaxDecodeRows = 512;
+
 // ----------------------------------------------------------------------------------- kernel probes
 // Live per-site timing for bench.py's roofline: HIP events recorded around every launch of a
 // probed site on the caller's stream (no synchronisation; read back after the timed region).
@@ -225,7 +229,7 @@ int decode_dup_mask() {
 }
 
 int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_elems, int M, int S_new, int past,
-               int max_blocks, hipStream_t s) {
+               int max_blocks, hipStream_t s, const int* anc = nullptr, int anc_ld = 0) {
   const int E = d->n_embd, H = d->n_head, L = d->n_layer;
   const int dup = S_new == 1 ? decode_dup_mask() : 0;
   const int dt = d->dtype;
@@ -250,9 +254,14 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     // pages are allocated contiguously per sequence (vcap_decode_init: identity table), so the bf16
     // short-context kernel computes page ids instead of loading them (nullptr table)
     const int* pt_arg = (dt == VCAP_DT_BF16 && past + S_new <= 64) ? nullptr : w.pt;
-    for (int r = 0; r < 1 + ((dup >> 1) & 1); ++r)
-      VCAP_TRY(vcap_decode_attention_dispatch(dt, w.q, a.kc, a.vc, pt_arg, maxp, w.attn, M, H, S_new, past, s),
-               "decode_attention");
+    for (int r = 0; r < 1 + ((dup >> 1) & 1); ++r) {
+      if (anc)   // beam search: keys through the ancestry table (one query row per sequence)
+        VCAP_TRY(vcap_decode_attention_anc_dispatch(dt, w.q, a.kc, a.vc, anc, anc_ld, maxp, w.attn, M, H, past, s),
+                 "decode_attention_anc");
+      else
+        VCAP_TRY(vcap_decode_attention_dispatch(dt, w.q, a.kc, a.vc, pt_arg, maxp, w.attn, M, H, S_new, past, s),
+                 "decode_attention");
+    }
     // 3) attn c_proj + residual
     RowsGemmArgs b;
     memset(&b, 0, sizeof(b));
@@ -385,6 +394,129 @@ std::string graph_key(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const 
   (void)hipGetDevice(&dev);
   put(&dev, sizeof(dev));
   return k;
+}
+
+// Replay the graph cached under `key`, capturing `issue(capture_stream)` into it first if absent.
+template <typename Issue>
+int launch_cached(const std::string& key, hipStream_t s, Issue issue) {
+  std::lock_guard<std::mutex> lk(g_graph_mu);
+  auto it = g_graphs.find(key);
+  if (it == g_graphs.end()) {
+    int dev = 0;
+    VCAP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    hipStream_t cs = g_capture_streams[dev];
+    if (!cs) {
+      VCAP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "hipStreamCreate");
+      g_capture_streams[dev] = cs;
+    }
+    VCAP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    int rc = issue(cs);
+    hipGraph_t graph = nullptr;
+    hipError_t ec = hipStreamEndCapture(cs, &graph);
+    if (rc) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    VCAP_TRY(ec, "hipStreamEndCapture");
+    GraphEntry ge;
+    hipError_t ei = hipGraphInstantiate(&ge.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    VCAP_TRY(ei, "hipGraphInstantiate");
+    if (hipError_t ee = hipEventCreateWithFlags(&ge.done, hipEventDisableTiming)) {
+      (void)hipGraphExecDestroy(ge.exec);
+      return hip_fail(ee, "hipEventCreate");
+    }
+    graph_cache_evict_to(graph_cache_cap() - 1);
+    g_graph_lru.push_front(key);
+    ge.lru = g_graph_lru.begin();
+    it = g_graphs.emplace(key, ge).first;
+  } else {
+    g_graph_lru.splice(g_graph_lru.begin(), g_graph_lru, it->second.lru);
+  }
+  VCAP_TRY(hipGraphLaunch(it->second.exec, s), "hipGraphLaunch");
+  VCAP_TRY(hipEventRecord(it->second.done, s), "hipEventRecord");
+  return 0;
+}
+
+// ----------------------------------------------------------------------------------- beam search
+struct BeamBufs {
+  DecBufs w;
+  int maxp;
+  size_t page_elems;
+  float* logits;
+  float* part_max;
+  float* part_sum;
+  BeamState st;
+  int nblk, chunks, anc_ld;
+};
+
+BeamBufs carve_beam(Carver& c, const vcap_gpt2_desc* d, int B, int nb, int S0, int L) {
+  BeamBufs b;
+  const int R = B * nb;
+  b.w = carve_dec(c, d, R, S0, L, &b.maxp, &b.page_elems);
+  b.nblk = max_logit_blocks(d->vocab, R);
+  b.chunks = vcap_beam_chunks(d->vocab);
+  b.anc_ld = S0 + L;
+  b.logits = (float*)c.take((size_t)R * d->vocab * 4);
+  b.part_max = (float*)c.take((size_t)R * b.nblk * 4);
+  b.part_sum = (float*)c.take((size_t)R * b.nblk * 4);
+  BeamState& st = b.st;
+  const size_t RL = (size_t)R * L * 4;
+  st.run_seq = (int*)c.take(RL);
+  st.run_bidx = (int*)c.take(RL);
+  st.seqs = (int*)c.take(RL);
+  st.beam_idx = (int*)c.take(RL);
+  st.run_score = (float*)c.take((size_t)R * 4);
+  st.beam_score = (float*)c.take((size_t)R * 4);
+  st.fin = (int*)c.take((size_t)R * 4);
+  st.unsat = (int*)c.take((size_t)B * 4);
+  st.stopped = (int*)c.take(4);
+  st.tok_next = (int*)c.take((size_t)R * 4);
+  st.anc = (int*)c.take((size_t)R * b.anc_ld * 4);
+  st.cand_val = (float*)c.take((size_t)R * b.chunks * 2 * nb * 4);
+  st.cand_tok = (int*)c.take((size_t)R * b.chunks * 2 * nb * 4);
+  return b;
+}
+
+int issue_beam(const vcap_gpt2_desc* d, const vcap_beam_params* bp, const float* prefix, const int* ids, int nids,
+               int B, int* out_ids, int* out_len, const BeamBufs& bb, hipStream_t s) {
+  const int E = d->n_embd, nb = bp->num_beams, L = bp->max_new_tokens, R = B * nb;
+  const int S0 = d->prefix_len + nids;
+  const DecBufs& w = bb.w;
+  auto lm_head = [&](int S_new) -> int {
+    RowsGemmArgs g;
+    memset(&g, 0, sizeof(g));
+    g.M = R; g.x = w.h + (size_t)(S_new - 1) * E; g.ldx = (long)S_new * E;
+    g.ln_g = d->lnf_g; g.ln_b = d->lnf_b; g.ln_eps = d->ln_eps;
+    g.w = d->lm_head; g.N = d->vocab; g.K = E;
+    g.logits_raw = bb.logits; g.part_val = bb.part_max; g.part_sum = bb.part_sum; g.nblk = bb.nblk;
+    VCAP_TRY(vcap_rows_gemm_dispatch(d->dtype, PRO_LN, EPI_LSE, g, nullptr, s), "lm_head_lse");
+    return 0;
+  };
+  VCAP_TRY(vcap_decode_init_dispatch(w.pt, R, bb.maxp, w.finished, w.nbanned, s), "decode_init");
+  // prefill: every beam row gets its sequence's prompt (HF expands the input to B * num_beams)
+  VCAP_TRY(vcap_prefill_embed_dispatch(d->dtype, prefix, d->prefix_len, ids, nids, d->wte, d->wpe, w.h, R, E, s, 0, nb),
+           "prefill_embed");
+  if (int rc = run_layers(d, w, bb.maxp, bb.page_elems, R * S0, S0, 0, 0, s)) return rc;
+  if (int rc = lm_head(S0)) return rc;
+  VCAP_TRY(vcap_beam_init_dispatch(bb.st, B, nb, L, S0, bb.anc_ld, bp->eos_token_id, s), "beam_init");
+  for (int cur = 0; cur < L; ++cur) {
+    if (cur > 0) {
+      const int pos = S0 + cur - 1;
+      VCAP_TRY(vcap_embed_tokens_dispatch(d->dtype, bb.st.tok_next, R, d->wte, d->wpe, w.h, E, pos, s), "embed");
+      if (int rc = run_layers(d, w, bb.maxp, bb.page_elems, R, 1, pos, 0, s, bb.st.anc, bb.anc_ld)) return rc;
+      if (int rc = lm_head(1)) return rc;
+    }
+    VCAP_TRY(vcap_beam_cand_dispatch(bb.st, bb.logits, bb.part_max, bb.part_sum, bb.nblk, R, d->vocab, nb, L, cur,
+                                     bp->repetition_penalty, bp->no_repeat_ngram_size, bp->min_new_tokens,
+                                     bp->eos_token_id, bb.chunks, s),
+             "beam_cand");
+    VCAP_TRY(vcap_beam_select_dispatch(bb.st, B, nb, L, d->vocab, bb.chunks, cur, bp->eos_token_id,
+                                       bp->length_penalty, S0, bb.anc_ld, s),
+             "beam_select");
+  }
+  VCAP_TRY(vcap_beam_output_dispatch(bb.st, B, nb, L, out_ids, out_len, s), "beam_output");
+  return 0;
 }
 
 }  // namespace
@@ -703,7 +835,8 @@ int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const
   if (gp->max_new_tokens > 64)
     return fail(VCAP_E_UNSUPPORTED, "max_new_tokens > 64 (the lm_head stages the processors' history in LDS)");
   const int S0 = d->prefix_len + prompt_len;
-  if (S0 <= 0 || B * S0 > 128) return fail(VCAP_E_UNSUPPORTED, "B*(prefix+prompt) must be <= 128 rows");
+  if (S0 <= 0 || B * S0 > kMaxDecodeRows)
+    return fail(VCAP_E_UNSUPPORTED, "B*(prefix+prompt) exceeds vcap_gpt2_max_rows()");
   if (S0 + gp->max_new_tokens > d->n_positions || S0 + gp->max_new_tokens > 1024)
     return fail(VCAP_E_UNSUPPORTED, "context exceeds n_positions");
   for (int i = 0; i < prompt_len; ++i)
@@ -719,43 +852,9 @@ int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const
     return issue_decode(d, gp, prefix, prompt_ids, prompt_len, B, out_ids, logits_out, w, maxp, page_elems, s);
 
   const std::string key = graph_key(d, gp, prefix, prompt_ids, prompt_len, B, out_ids, logits_out, workspace);
-  std::lock_guard<std::mutex> lk(g_graph_mu);
-  auto it = g_graphs.find(key);
-  if (it == g_graphs.end()) {
-    int dev = 0;
-    VCAP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    hipStream_t cs = g_capture_streams[dev];
-    if (!cs) {
-      VCAP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "hipStreamCreate");
-      g_capture_streams[dev] = cs;
-    }
-    VCAP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-    int rc = issue_decode(d, gp, prefix, prompt_ids, prompt_len, B, out_ids, logits_out, w, maxp, page_elems, cs);
-    hipGraph_t graph = nullptr;
-    hipError_t ec = hipStreamEndCapture(cs, &graph);
-    if (rc) {
-      if (graph) (void)hipGraphDestroy(graph);
-      return rc;
-    }
-    VCAP_TRY(ec, "hipStreamEndCapture");
-    GraphEntry ge;
-    hipError_t ei = hipGraphInstantiate(&ge.exec, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    VCAP_TRY(ei, "hipGraphInstantiate");
-    if (hipError_t ee = hipEventCreateWithFlags(&ge.done, hipEventDisableTiming)) {
-      (void)hipGraphExecDestroy(ge.exec);
-      return hip_fail(ee, "hipEventCreate");
-    }
-    graph_cache_evict_to(graph_cache_cap() - 1);
-    g_graph_lru.push_front(key);
-    ge.lru = g_graph_lru.begin();
-    it = g_graphs.emplace(key, ge).first;
-  } else {
-    g_graph_lru.splice(g_graph_lru.begin(), g_graph_lru, it->second.lru);
-  }
-  VCAP_TRY(hipGraphLaunch(it->second.exec, s), "hipGraphLaunch");
-  VCAP_TRY(hipEventRecord(it->second.done, s), "hipEventRecord");
-  return 0;
+  return launch_cached(key, s, [&](hipStream_t cs) {
+    return issue_decode(d, gp, prefix, prompt_ids, prompt_len, B, out_ids, logits_out, w, maxp, page_elems, cs);
+  });
 }
 
 int vcap_probe_enable(const char* site, int max_launches) {
@@ -807,7 +906,7 @@ size_t vcap_gpt2_beam_workspace_bytes(const vcap_gpt2_desc* d, int rows, int S0,
 static int step_setup(const vcap_gpt2_desc* d, int rows, int S0, int max_new, void* ws, size_t ws_bytes, DecBufs* w,
                       int* maxp, size_t* pe, void** scratch) {
   if (int rc = check_gpt2_launch(d)) return rc;
-  if (rows <= 0 || rows > 128 || S0 <= 0 || max_new <= 0 || S0 + max_new > d->n_positions)
+  if (rows <= 0 || rows > kMaxDecodeRows || S0 <= 0 || max_new <= 0 || S0 + max_new > d->n_positions)
     return fail(VCAP_E_ARG, "gpt2 step: bad rows / lengths");
   if (ws_bytes < vcap_gpt2_beam_workspace_bytes(d, rows, S0, max_new))
     return fail(VCAP_E_WORKSPACE, "gpt2 step: workspace too small (vcap_gpt2_beam_workspace_bytes)");
@@ -823,7 +922,7 @@ int vcap_gpt2_prefill(const vcap_gpt2_desc* d, const float* prefix, const int* p
   const int S0 = d ? d->prefix_len + prompt_len : 0;
   if (!prefix || !logits_out || B <= 0 || B > rows || prompt_len < 0 || prompt_len > 64 || (prompt_len && !prompt_ids))
     return fail(VCAP_E_ARG, "vcap_gpt2_prefill: bad arguments");
-  if (B * S0 > 128) return fail(VCAP_E_UNSUPPORTED, "B*(prefix+prompt) must be <= 128 rows");
+  if (B * S0 > kMaxDecodeRows) return fail(VCAP_E_UNSUPPORTED, "B*(prefix+prompt) exceeds vcap_gpt2_max_rows()");
   DecBufs w;
   int maxp;
   size_t pe;
@@ -861,7 +960,8 @@ int vcap_gpt2_forward_embeds(const vcap_gpt2_desc* d, const float* embeds, int r
   if (past_len == 0 ? n_tok != S0 : (n_tok != 1 || past_len < S0 || past_len >= S0 + max_new_tokens))
     return fail(VCAP_E_ARG, "vcap_gpt2_forward_embeds: prefill needs n_tok == S0; a step one token at "
                             "S0 <= past_len < S0 + max_new_tokens");
-  if (past_len == 0 && rows * S0 > 128) return fail(VCAP_E_UNSUPPORTED, "rows*S0 must be <= 128 at prefill");
+  if (past_len == 0 && rows * S0 > kMaxDecodeRows)
+    return fail(VCAP_E_UNSUPPORTED, "rows*S0 exceeds vcap_gpt2_max_rows() at prefill");
   DecBufs w;
   int maxp;
   size_t pe;
@@ -917,6 +1017,59 @@ void vcap_graph_cache_clear(void) {
   graph_cache_evict_to(0);
   g_graphs.clear();
   g_graph_lru.clear();
+}
+
+int vcap_gpt2_max_rows(void) { return kMaxDecodeRows; }
+
+size_t vcap_gpt2_beam_search_workspace_bytes(const vcap_gpt2_desc* d, int B, int num_beams, int S0,
+                                             int max_new_tokens) {
+  if (check_gpt2(d) || B <= 0 || num_beams <= 0) return 0;
+  Carver c(nullptr);
+  carve_beam(c, d, B, num_beams, S0, max_new_tokens);
+  return c.off;
+}
+
+int vcap_gpt2_beam_search(const vcap_gpt2_desc* d, const vcap_beam_params* bp, const float* prefix,
+                          const int* prompt_ids, int prompt_len, int B, int* out_ids, int* out_len, void* workspace,
+                          size_t ws_bytes, void* stream) {
+  if (int rc = check_gpt2_launch(d)) return rc;
+  if (!bp || !prefix || !out_ids || !out_len || B <= 0 || prompt_len < 0 || prompt_len > 64 ||
+      (prompt_len && !prompt_ids))
+    return fail(VCAP_E_ARG, "vcap_gpt2_beam_search: bad arguments");
+  const int nb = bp->num_beams, L = bp->max_new_tokens, S0 = d->prefix_len + prompt_len;
+  if (nb < 2 || nb > 8 || B > 16 || L <= 0 || L > 64 || S0 + L > 72 || S0 + L > d->n_positions)
+    return fail(VCAP_E_UNSUPPORTED, "vcap_gpt2_beam_search: needs 2 <= num_beams <= 8, B <= 16, max_new <= 64, "
+                                    "prefix + prompt + max_new <= 72");
+  if (B * nb * S0 > kMaxDecodeRows) return fail(VCAP_E_UNSUPPORTED, "B*num_beams*(prefix+prompt) exceeds max rows");
+  if (bp->early_stopping != 0) return fail(VCAP_E_UNSUPPORTED, "only early_stopping=False (the reference's presets)");
+  if (nb * vcap_beam_chunks(d->vocab) * 2 * nb > 20 * 64)
+    return fail(VCAP_E_UNSUPPORTED, "num_beams too large for the vocabulary (candidate registers)");
+  for (int i = 0; i < prompt_len; ++i)
+    if (prompt_ids[i] < 0 || prompt_ids[i] >= d->vocab) return fail(VCAP_E_ARG, "prompt id out of range");
+  if (ws_bytes < vcap_gpt2_beam_search_workspace_bytes(d, B, nb, S0, L))
+    return fail(VCAP_E_WORKSPACE, "vcap_gpt2_beam_search: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  Carver c(workspace);
+  BeamBufs bb = carve_beam(c, d, B, nb, S0, L);
+  if (!bp->use_graph) return issue_beam(d, bp, prefix, prompt_ids, prompt_len, B, out_ids, out_len, bb, s);
+  std::string key = "beam";
+  auto put = [&](const void* p, size_t n) { key.append((const char*)p, n); };
+  put(d, sizeof(*d));
+  for (int l = 0; l < d->n_layer; ++l) put(&d->layers[l], sizeof(vcap_gpt2_layer));
+  put(bp, sizeof(*bp));
+  put(&prefix, sizeof(prefix));
+  put(prompt_ids, sizeof(int) * (size_t)prompt_len);
+  put(&prompt_len, sizeof(prompt_len));
+  put(&B, sizeof(B));
+  put(&out_ids, sizeof(out_ids));
+  put(&out_len, sizeof(out_len));
+  put(&workspace, sizeof(workspace));
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  put(&dev, sizeof(dev));
+  return launch_cached(key, s, [&](hipStream_t cs) {
+    return issue_beam(d, bp, prefix, prompt_ids, prompt_len, B, out_ids, out_len, bb, cs);
+  });
 }
 
 int vcap_graph_cache_size(void) {

@@ -22,7 +22,9 @@ struct GemmEpi {
 };
 
 enum { PRO_LN = 0, PRO_DIRECT = 1 };
-enum { EPI_QKV = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_LOGITS = 3, EPI_STORE = 4 };
+// EPI_LSE: raw logits -> logits_raw + per-workgroup (max, sum exp(x - max)) partials per row
+// (part_val / part_sum): the log_softmax statistics of beam search
+enum { EPI_QKV = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_LOGITS = 3, EPI_STORE = 4, EPI_LSE = 5 };
 
 struct RowsGemmArgs {
   const void* x;  // PRO_LN: f32 residual rows; PRO_DIRECT: T rows
@@ -45,6 +47,7 @@ struct RowsGemmArgs {
   float* logits_raw;  // optional [M, N] raw logits
   float* part_val;
   int* part_idx;
+  float* part_sum;  // EPI_LSE
   int nblk;
   const int* hist;  // [M][hist_ld] generated tokens
   int hist_ld, gen_len;
@@ -93,7 +96,8 @@ int vcap_logit_blocks(int V, int M);
 hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc, const void* vc, const int* pt,
                                           int maxp, void* out, int M, int H, int S_new, int past, hipStream_t s);
 hipError_t vcap_prefill_embed_dispatch(int dt, const float* prefix, int P, const int* ids, int nids, const void* wte,
-                                       const float* wpe, float* h, int B, int E, hipStream_t s, int pos0 = 0);
+                                       const float* wpe, float* h, int B, int E, hipStream_t s, int pos0 = 0,
+                                       int prefix_rep = 1);
 hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s);
 hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const int* part_idx, int nblk, int B,
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
@@ -101,6 +105,38 @@ hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const in
                                          const float* wpe, float* h, int E, int pos_next, int vocab, hipStream_t s);
 hipError_t vcap_embed_tokens_dispatch(int dt, const int* tok, int rows, const void* wte, const float* wpe, float* h,
                                       int E, int pos, hipStream_t s);
+// ---- device beam search (csrc/beam.hip) ----
+struct BeamState {  // per-call device state, carved from the caller's workspace (B batches, nb beams, L = max_new)
+  int* run_seq;      // [B][nb][L] running hypotheses' tokens
+  float* run_score;  // [B][nb]
+  int* run_bidx;     // [B][nb][L] beam indices (HF running_beam_indices)
+  int* seqs;         // [B][nb][L] finished hypotheses (EOS-initialised)
+  float* beam_score; // [B][nb] (-1e9 initialised)
+  int* beam_idx;     // [B][nb][L] (-1 initialised)
+  int* fin;          // [B][nb]
+  int* unsat;        // [B]
+  int* stopped;      // [1] HF's loop has ended (no further updates)
+  int* tok_next;     // [B*nb] next input tokens
+  int* anc;          // [B*nb][anc_ld] physical row holding each position's K/V
+  float* cand_val;   // [B*nb][C][2nb]
+  int* cand_tok;
+};
+hipError_t vcap_beam_init_dispatch(const BeamState& st, int B, int nb, int L, int S0, int anc_ld, int eos,
+                                   hipStream_t s);
+hipError_t vcap_beam_cand_dispatch(const BeamState& st, const float* logits, const float* part_max,
+                                   const float* part_sum, int nblk, int rows, int V, int nb, int L, int cur,
+                                   float rep, int ngram, int min_new, int eos, int chunks, hipStream_t s);
+hipError_t vcap_beam_select_dispatch(const BeamState& st, int B, int nb, int L, int V, int chunks, int cur, int eos,
+                                     float length_penalty, int S0, int anc_ld, hipStream_t s);
+hipError_t vcap_beam_output_dispatch(const BeamState& st, int B, int nb, int L, int* out_ids, int* out_len,
+                                     hipStream_t s);
+int vcap_beam_chunks(int V);
+// causal decode attention (one query row per sequence) whose key j of row m lives in physical
+// row anc[m * anc_ld + j] of the contiguous-page pools (beam search: no KV copies on reorder)
+hipError_t vcap_decode_attention_anc_dispatch(int dt, const void* q, const void* kc, const void* vc, const int* anc,
+                                              int anc_ld, int maxp, void* out, int M, int H, int past,
+                                              hipStream_t s);
+
 hipError_t vcap_kv_gather_dispatch(int dt, const void* src_pool, void* dst_pool, const int* src_rows, int rows, int maxp,
                                    int H, int len, long layer_elems, int L, hipStream_t s);
 size_t vcap_frames_ws_bytes(int n, int in_h, int in_w, int out_h, int out_w);

@@ -61,6 +61,12 @@ class GenParams(C.Structure):
                 ("max_blocks", i32)]
 
 
+class BeamParams(C.Structure):
+    _fields_ = [("num_beams", i32), ("max_new_tokens", i32), ("min_new_tokens", i32),
+                ("no_repeat_ngram_size", i32), ("repetition_penalty", f32), ("length_penalty", f32),
+                ("early_stopping", i32), ("eos_token_id", i32), ("use_graph", i32)]
+
+
 # name -> (restype, argtypes); every symbol include/vcap.h declares
 SIGNATURES = {
     "vcap_last_error": (C.c_char_p, []),
@@ -92,6 +98,10 @@ SIGNATURES = {
                                  vp, vp, sz, vp]),
     "vcap_graph_cache_clear": (None, []),
     "vcap_graph_cache_size": (i32, []),
+    "vcap_gpt2_max_rows": (i32, []),
+    "vcap_gpt2_beam_search_workspace_bytes": (sz, [C.POINTER(GPT2Desc), i32, i32, i32, i32]),
+    "vcap_gpt2_beam_search": (i32, [C.POINTER(GPT2Desc), C.POINTER(BeamParams), vp, C.POINTER(C.c_int), i32, i32,
+                                    vp, vp, vp, sz, vp]),
     "vcap_decode_attention": (i32, [i32, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, vp]),
     "vcap_gpt2_beam_workspace_bytes": (sz, [C.POINTER(GPT2Desc), i32, i32, i32]),
     "vcap_gpt2_prefill": (i32, [C.POINTER(GPT2Desc), vp, C.POINTER(C.c_int), i32, i32, i32, i32, vp, vp, sz, vp]),

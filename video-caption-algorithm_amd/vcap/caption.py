@@ -151,10 +151,11 @@ class HipTextDecoder:
             return trim_generated(ids, eos)
         from . import search
         if num_beams > 1:
-            return search.beam_search(self.hip, prefix, prompt_ids, num_beams=num_beams,
-                                      max_new_tokens=max_new_tokens, min_new_tokens=min_new_tokens,
-                                      no_repeat_ngram_size=no_repeat_ngram_size,
-                                      repetition_penalty=repetition_penalty, eos=eos)
+            return search.beam_search_device(self.hip, prefix, prompt_ids, num_beams=num_beams,
+                                             max_new_tokens=max_new_tokens, min_new_tokens=min_new_tokens,
+                                             no_repeat_ngram_size=no_repeat_ngram_size,
+                                             repetition_penalty=repetition_penalty, eos=eos,
+                                             use_graph=self.use_graph)
         return search.sample(self.hip, prefix, prompt_ids, temperature=temperature, top_p=top_p,
                              max_new_tokens=max_new_tokens, min_new_tokens=min_new_tokens,
                              no_repeat_ngram_size=no_repeat_ngram_size, repetition_penalty=repetition_penalty,

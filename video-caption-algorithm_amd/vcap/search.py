@@ -3,6 +3,9 @@
 The forward passes (prefill, one token per row per step, KV-cache row permutation) run in
 libvcap_hip.so; this module keeps the search bookkeeping as small device tensor ops.
 
+`beam_search_device` runs the whole search in libvcap_hip.so (csrc/beam.hip, one hipGraph); the
+host-bookkeeping `beam_search` below is its cross-check (tests/test_gpu_search.py).
+
 Beam search restates transformers 5.15.0 `GenerationMixin._beam_search` (the only copy in this
 image; the reference pins 4.57.1) as the reference reaches it from
 text_decoder.py:131-144 with inputs_embeds (decoder_prompt_len = 0): log_softmax -> processors
@@ -51,6 +54,45 @@ class _StepState:
         N.check(N.lib().vcap_gpt2_reorder(C.byref(self.dec.desc), src.data_ptr(), self.rows, self.S0, self.max_new,
                                           length, self.ws.data_ptr(), self.ws.numel(), self.stream),
                 "vcap_gpt2_reorder")
+
+
+@torch.no_grad()
+def beam_search_device(dec, prefix: torch.Tensor, prompt_ids: Sequence[int], *, num_beams: int, max_new_tokens: int,
+                       min_new_tokens: int = 8, no_repeat_ngram_size: int = 3, repetition_penalty: float = 1.1,
+                       eos: int = 50256, length_penalty: float = 1.0, use_graph: bool = True) -> List[List[int]]:
+    """The same search as `beam_search`, entirely on the device (vcap_gpt2_beam_search: fused
+    log_softmax / processor / top-2k kernels and a device bookkeeping kernel, one hipGraph, one
+    device->host copy of the result).  Persistent per-shape buffers keep the captured graph."""
+    B, P, E = prefix.shape
+    dev = prefix.device
+    ids = [int(i) for i in prompt_ids]
+    S0 = dec.prefix_len + len(ids)
+    cache = dec.__dict__.setdefault("_beam_bufs", {})   # persistent per decoder and shape
+    key = (B, P, E, num_beams, max_new_tokens)
+    if key not in cache:
+        nbytes = int(N.lib().vcap_gpt2_beam_search_workspace_bytes(C.byref(dec.desc), B, num_beams, S0, max_new_tokens))
+        if nbytes == 0:
+            raise ValueError("vcap_gpt2_beam_search_workspace_bytes: unsupported shape")
+        cache[key] = {"pre": torch.empty(B, P, E, dtype=torch.float32, device=dev),
+                           "ids": torch.empty(B, max_new_tokens, dtype=torch.int32, device=dev),
+                           "len": torch.empty(B, dtype=torch.int32, device=dev), "ws": {}}
+    bufs = cache[key]
+    nbytes = int(N.lib().vcap_gpt2_beam_search_workspace_bytes(C.byref(dec.desc), B, num_beams, S0, max_new_tokens))
+    ws = bufs["ws"].get(S0)
+    if ws is None or ws.numel() < nbytes:
+        ws = bufs["ws"][S0] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    bufs["pre"].copy_(prefix)
+    bp = N.BeamParams(num_beams=int(num_beams), max_new_tokens=int(max_new_tokens),
+                      min_new_tokens=int(min_new_tokens), no_repeat_ngram_size=int(no_repeat_ngram_size),
+                      repetition_penalty=float(repetition_penalty), length_penalty=float(length_penalty),
+                      early_stopping=0, eos_token_id=int(eos), use_graph=int(bool(use_graph)))
+    arr = (C.c_int * max(len(ids), 1))(*ids)
+    N.check(N.lib().vcap_gpt2_beam_search(C.byref(dec.desc), C.byref(bp), bufs["pre"].data_ptr(), arr, len(ids), B,
+                                          bufs["ids"].data_ptr(), bufs["len"].data_ptr(), ws.data_ptr(), ws.numel(),
+                                          torch.cuda.current_stream(dev).cuda_stream), "vcap_gpt2_beam_search")
+    out = bufs["ids"].cpu()
+    n = int(bufs["len"].max().item())
+    return [list(map(int, r)) for r in out[:, :n].tolist()]
 
 
 def _processors(scores: torch.Tensor, seqs: torch.Tensor, rep: float, ngram: int, min_new: int, eos: int):

@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp8"],
                     help="fp8: MXFP8 ViT QKV/fc1/fc2 GEMMs (BASELINE configs[4]); the decoder stays bf16")
     ap.add_argument("--decode", default="hf_greedy", choices=["hf_greedy", "raw_greedy"])
+    ap.add_argument("--beams", type=int, default=1,
+                    help=">1: device beam search (preset detailed = 4 beams / max_new 40: BASELINE configs[3])")
     ap.add_argument("--vit", default="vit_base_patch16_224")
     ap.add_argument("--gpt2", default="gpt2")
     ap.add_argument("--no-graph", action="store_true")
@@ -88,7 +90,7 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(sd, va, ga, frames_np, budget_s: float, max_new: int):
+def cpu_baseline(sd, va, ga, frames_np, budget_s: float, max_new: int, beams: int = 1):
     """Time the CPU oracle (fp32) on ONE video at a time (the reference's single-video CPU path):
     p50 over >= 5 captions after one warm-up caption."""
     import torch
@@ -100,21 +102,23 @@ def cpu_baseline(sd, va, ga, frames_np, budget_s: float, max_new: int):
     with torch.no_grad():
         while True:
             t0 = time.perf_counter()
-            ids = O.caption_ids(sd, va, ga, video, [ga.bos_token_id], max_new_tokens=max_new)
+            ids = O.caption_ids(sd, va, ga, video, [ga.bos_token_id], max_new_tokens=max_new, num_beams=beams)
             times.append(time.perf_counter() - t0)
             if (time.perf_counter() - t_start > budget_s and len(times) >= 6) or len(times) >= 8:
                 break
     p50 = statistics.median(times[1:] if len(times) > 1 else times)
     out = {"value": 1.0 / p50, "unit": "captions/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
-           "sample": f"{len(times)} single-video captions (1x16x3x224x224, fp32 torch CPU oracle, HF-greedy "
-                     f"max_new {max_new}); p50 of runs after the first = {p50 * 1e3:.0f} ms",
+           "sample": f"{len(times)} single-video captions (1x{frames_np.shape[1]}x3x{va.image}x{va.image}, fp32 torch "
+                     f"CPU oracle, {'HF-greedy' if beams == 1 else f'HF beam {beams}'} max_new {max_new}); p50 of "
+                     f"runs after the first = {p50 * 1e3:.0f} ms",
            "p50_latency_ms": p50 * 1e3, "tokens_first": [int(t) for t in ids[0][:4]]}
     # one batch of all the workload's videos (B in {1, 8}) when the budget allows it
     B = frames_np.shape[0]
     if B > 1 and time.perf_counter() - t_start < budget_s:
         with torch.no_grad():
             t0 = time.perf_counter()
-            O.caption_ids(sd, va, ga, torch.from_numpy(frames_np), [ga.bos_token_id], max_new_tokens=max_new)
+            O.caption_ids(sd, va, ga, torch.from_numpy(frames_np), [ga.bos_token_id], max_new_tokens=max_new,
+                          num_beams=beams)
             tb = time.perf_counter() - t0
         out["batch"] = {"videos": B, "seconds": tb, "captions_per_s": B / tb}
     return out
@@ -156,10 +160,11 @@ def decode_step_alone(dec, prefix, ids_cfg, ga):
     replayed after warm-up (the prefill cancels)."""
     import torch
     from vcap.model import GenConfig
+    import dataclasses
     res = {}
-    for mx in (1, ids_cfg.max_new_tokens):
-        cfg = GenConfig(mx, ids_cfg.min_new_tokens, ids_cfg.no_repeat_ngram_size, ids_cfg.repetition_penalty,
-                        ga.eos_token_id, ga.eos_token_id, True)
+    lo = 2 if ids_cfg.num_beams > 1 else 1
+    for mx in (lo, ids_cfg.max_new_tokens):
+        cfg = dataclasses.replace(ids_cfg, max_new_tokens=mx, use_graph=True, max_blocks=0)
         out = torch.empty(prefix.shape[0], mx, dtype=torch.int32, device=prefix.device)
         for _ in range(3):
             dec.generate_ids(prefix, [ga.bos_token_id], cfg, out=out)
@@ -169,7 +174,7 @@ def decode_step_alone(dec, prefix, ids_cfg, ga):
             dec.generate_ids(prefix, [ga.bos_token_id], cfg, out=out)
         torch.cuda.synchronize()
         res[mx] = (time.perf_counter() - t) / 20
-    return (res[ids_cfg.max_new_tokens] - res[1]) / (ids_cfg.max_new_tokens - 1), res[1]
+    return (res[ids_cfg.max_new_tokens] - res[lo]) / (ids_cfg.max_new_tokens - lo), res[lo]
 
 
 def token_agreement(got, ref):
@@ -182,6 +187,14 @@ def token_agreement(got, ref):
         lead.append(n / len(b))
     return sum(lead) / len(lead), sum(int(x == y) for a, b in zip(got, ref) for x, y in zip(a, b)) / (
         len(ref) * len(ref[0]))
+
+
+def workload_tag(args, world):
+    if args.precision == "fp8":
+        return "configs[4]-shaped, MXFP8 ViT GEMMs"
+    if args.vit == "vit_large_patch14_224" and args.gpt2 == "gpt2-medium" and args.beams > 1:
+        return "configs[3]"
+    return "configs[1]" + ("/[2]" if world > 1 else "")
 
 
 def main():
@@ -223,7 +236,8 @@ def main():
     pre = HipPrefix(sd, ga.n_embd, device=dev)
     dec = HipGPT2Decoder(sd, ga, "bf16" if args.precision == "fp8" else args.precision, dev)
     if args.decode == "hf_greedy":
-        cfg = GenConfig(args.max_new, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, not args.no_graph)
+        cfg = GenConfig(args.max_new, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, not args.no_graph,
+                        num_beams=args.beams)
     else:
         cfg = GenConfig.raw_greedy(args.max_new, ga.eos_token_id, not args.no_graph)
     cfg.max_blocks = 0 if args.serial else args.decode_blocks
@@ -321,12 +335,11 @@ def main():
     if args.decode_alone:
         with torch.cuda.stream(torch.cuda.Stream(dev)):
             _, pre_a = enc.encode(video, pre)
-            cfg_a = GenConfig(args.max_new, cfg.min_new_tokens, cfg.no_repeat_ngram_size, cfg.repetition_penalty,
-                              ga.eos_token_id, ga.eos_token_id, True)
-            step_s, prefill_s = decode_step_alone(dec, pre_a, cfg_a, ga)
+            step_s, prefill_s = decode_step_alone(dec, pre_a, cfg, ga)
         wbytes = ga.weight_elems_per_step() * (4 if args.precision == "fp32" else 2)
-        dec_alone = {"what": "one token step of the B-row greedy decode graph, alone on the GPU "
-                             "((24-step - 1-step graph) / 23)",
+        dec_alone = {"what": (f"one token step of the B-row greedy decode graph" if args.beams == 1 else
+                              f"one step of the device beam search graph ({B} x {args.beams} beams)") +
+                             ", alone on the GPU (difference of a max_new-step and a 1-2-step graph)",
                      "step_us": step_s * 1e6, "prefill_plus_one_step_us": prefill_s * 1e6,
                      "weight_bytes_per_step": wbytes, "achieved_gbs": wbytes / step_s / 1e9,
                      "frac_of_hbm_peak": wbytes / step_s / 1e9 / PEAK_HBM_GBS}
@@ -367,8 +380,9 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": {"bf16": "bf16", "fp8": "mxfp8-e4m3 (ViT QKV/proj/fc1/fc2) + bf16"}.get(args.precision, "f32"),
             "data": "synthetic (seeded U[0,1) frames, ImageNet-normalised; seeded random-init weights)",
             "config": {"workload": f"batch={B} synthetic {T}x3x224x224 videos per GPU, {args.vit} + {args.gpt2}, "
-                                   f"{args.decode} decode max_new {args.max_new} (BASELINE "
-                                   f"{'configs[4]-shaped, MXFP8 ViT GEMMs' if args.precision == 'fp8' else 'configs[1]' + ('/[2]' if world > 1 else '')})",
+                                   f"{args.decode if args.beams == 1 else f'beam-{args.beams}'} decode max_new {args.max_new} "
+                                   f"(BASELINE {workload_tag(args, world)})",
+                       "num_beams": args.beams,
                        "vit": args.vit, "gpt2": args.gpt2, "batch_per_gpu": B, "global_batch": world * B,
                        "frames": T, "max_new_tokens": args.max_new, "decode": args.decode,
                        "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}",
@@ -421,7 +435,7 @@ def main():
                                "what": "pinned host fp32 frames -> H2D -> encode -> decode -> ids on host, "
                                        "one batch at a time (no overlap; rank 0's clock)"}
         if world == 1 and args.cpu_baseline_s > 0:
-            out["cpu_baseline"] = cpu_baseline(sd, va, ga, frames_np, args.cpu_baseline_s, args.max_new)
+            out["cpu_baseline"] = cpu_baseline(sd, va, ga, frames_np, args.cpu_baseline_s, args.max_new, args.beams)
             out["cpu_baseline"].pop("tokens_first", None)
         else:
             out["cpu_baseline"] = None

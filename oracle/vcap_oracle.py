@@ -267,6 +267,64 @@ def generate_raw_greedy(sd, arch, inputs_embeds: Tensor, *, max_new_tokens: int 
     return out
 
 
+def generate_beam(sd, arch, inputs_embeds: Tensor, *, num_beams: int, max_new_tokens: int, min_new_tokens: int = 8,
+                  repetition_penalty: float = 1.1, no_repeat_ngram_size: int = 3, length_penalty: float = 1.0,
+                  eos_token_id: Optional[int] = None) -> List[List[int]]:
+    """HF GenerationMixin._beam_search (transformers 5.15.0 generation/utils.py, as
+    text_decoder.py:131-144 reaches it with inputs_embeds: prompt length 0, early_stopping False)
+    restated on the CPU: log_softmax -> processors -> + running beam scores -> top-2k over
+    beams x vocab -> running / finished updates -> cache reorder; stop when no batch can improve
+    or every candidate hit EOS / max length.  Returns each sequence's best finished hypothesis
+    (the first max(length) tokens, EOS-padded) - pinned to the reference's beam3 / beam4 goldens
+    (tests/test_cpu_oracle.py)."""
+    eos = arch.eos_token_id if eos_token_id is None else eos_token_id
+    B, nb = inputs_embeds.shape[0], num_beams
+    V, L, K = arch.vocab, max_new_tokens, 2 * num_beams
+    cache = KVCache(arch.n_layer)
+    wte = _t(sd, "decoder.model.transformer.wte.weight")
+    logits = gpt2_forward(sd, arch, inputs_embeds, cache)[:, -1, :].float().repeat_interleave(nb, dim=0)
+    cache.reorder(torch.arange(B * nb) // nb)
+    run_seq = torch.full((B, nb, L), eos, dtype=torch.long)
+    run_score = torch.zeros(B, nb)
+    run_score[:, 1:] = -1e9
+    run_bidx = torch.full((B, nb, L), -1, dtype=torch.long)
+    seqs, beam_idx = run_seq.clone(), run_bidx.clone()
+    beam_score = torch.full((B, nb), -1e9)
+    fin = torch.zeros(B, nb, dtype=torch.bool)
+    unsat = torch.ones(B, dtype=torch.bool)
+    take = lambda t, i: torch.stack([t[b][i[b]] for b in range(B)])  # noqa: E731
+    for cur in range(L):
+        lp = torch.log_softmax(logits, dim=-1)
+        lp = process_logits(lp, run_seq[:, :, :cur].reshape(B * nb, cur), repetition_penalty=repetition_penalty,
+                            no_repeat_ngram_size=no_repeat_ngram_size, min_new_tokens=min_new_tokens,
+                            eos_token_id=eos)
+        lp = (lp.view(B, nb, V) + run_score[:, :, None]).reshape(B, nb * V)
+        top_lp, top_i = torch.topk(lp, K)
+        src, tok = top_i // V, top_i % V
+        t_seq, t_bidx = take(run_seq, src), take(run_bidx, src)
+        t_seq[:, :, cur] = tok
+        t_bidx[:, :, cur] = src + torch.arange(B)[:, None] * nb
+        hits = (tok == eos) | (cur + 1 >= L)
+        run_lp = top_lp + hits.float() * -1.0e9
+        nxt = torch.topk(run_lp, nb)[1]
+        run_seq, run_score, run_bidx = take(t_seq, nxt), take(run_lp, nxt), take(t_bidx, nxt)
+        did = hits & (torch.arange(K) < nb)[None, :]
+        sc = top_lp / ((cur + 1) ** length_penalty)
+        sc = sc + (~unsat)[:, None].float() * -1.0e9 + (~did).float() * -1.0e9
+        m_sc, sel = torch.topk(torch.cat([beam_score, sc], 1), nb)
+        seqs, beam_idx = take(torch.cat([seqs, t_seq], 1), sel), take(torch.cat([beam_idx, t_bidx], 1), sel)
+        fin, beam_score = take(torch.cat([fin, did], 1), sel), m_sc
+        cache.reorder(run_bidx[:, :, cur].reshape(-1))
+        best_running = run_score[:, 0] / ((cur + 1) ** length_penalty)
+        worst = torch.where(fin, beam_score.min(dim=1, keepdim=True)[0], torch.full_like(beam_score, -1.0e9))
+        unsat = unsat & (best_running[:, None] > worst).any(dim=1)
+        if not bool(unsat.any()) or bool(hits.all()):
+            break
+        logits = gpt2_forward(sd, arch, wte[run_seq[:, :, cur].reshape(-1)].unsqueeze(1), cache)[:, -1, :].float()
+    n = int((beam_idx[:, 0, :] != -1).sum(dim=1).max())
+    return seqs[:, 0, :n].tolist()
+
+
 def caption_ids(sd, vit_arch, gpt_arch, video: Tensor, prompt_ids: Sequence[int], *, ln_scale: float = 0.6,
                 in_weight: float = 0.4, prefix_len: int = 4, mode: str = "hf_greedy", **gen_kw):
     """Engine path A1 (core/engine.py:39-64) up to token ids (before detokenize/clean_text)."""
@@ -276,6 +334,9 @@ def caption_ids(sd, vit_arch, gpt_arch, video: Tensor, prompt_ids: Sequence[int]
     x = build_inputs(sd, gpt_arch, pre, prompt_ids)
     if mode == "raw_greedy":
         return generate_raw_greedy(sd, gpt_arch, x, **gen_kw)
+    if gen_kw.get("num_beams", 1) > 1:
+        return torch.tensor(generate_beam(sd, gpt_arch, x, **gen_kw))
+    gen_kw.pop("num_beams", None)
     ids, _ = generate_greedy(sd, gpt_arch, x, **gen_kw)
     return ids
 

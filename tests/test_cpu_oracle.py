@@ -176,3 +176,24 @@ def test_oracle_pil_resize_matches_pillow(hw):
                 (np.add.outer(np.arange(h), 3 * np.arange(w))[:, :, None] * np.array([1, 2, 5]) % 256).astype(np.uint8)):
         ref = np.asarray(Image.fromarray(img).resize((224, 224), Image.BILINEAR))
         assert np.array_equal(O.pil_resize_bilinear(img, 224, 224), ref)
+
+
+@pytest.mark.parametrize("name,nb,mx", [("tiny", 3, 24), ("tiny", 4, 40), ("tiny_prompt", 3, 24)])
+def test_oracle_beam_matches_reference(name, nb, mx):
+    """The oracle's HF beam-search restatement (presets precise / detailed) reproduces the
+    reference's beam ids from the recorded prefix."""
+    meta, g, va, ga, sd, frames = case(name)
+    x = torch.from_numpy(g["inputs_embeds"].copy())
+    with torch.no_grad():
+        rows = O.generate_beam(sd, ga, x, num_beams=nb, max_new_tokens=mx)
+    assert np.array_equal(np.array(rows, dtype=np.int32), g[f"beam{nb}_ids"])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("nb,mx", [(3, 24), (4, 40)])
+def test_oracle_beam_matches_reference_b16_b2(nb, mx):
+    meta, g, va, ga, sd, frames = case("b16_b2")
+    x = torch.from_numpy(g["inputs_embeds"].copy())
+    with torch.no_grad():
+        rows = O.generate_beam(sd, ga, x, num_beams=nb, max_new_tokens=mx)
+    assert np.array_equal(np.array(rows, dtype=np.int32), g[f"beam{nb}_ids"])

@@ -55,6 +55,7 @@ __global__ void vcap_beam_init_kernel(BeamState st, int B, int nb, int L, int S0
 
 // ---------------------------------------------------------------------------------------------
 // Candidates of one (row, vocab chunk): processed log-prob + running score, top-2nb of the chunk.
+template <int K>
 __global__ __launch_bounds__(256) void vcap_beam_cand_kernel(BeamState st, const float* __restrict__ logits,
                                                              const float* __restrict__ part_max,
                                                              const float* __restrict__ part_sum, int nblk, int V,
@@ -63,12 +64,11 @@ __global__ __launch_bounds__(256) void vcap_beam_cand_kernel(BeamState st, const
   __shared__ float s_red[8];
   __shared__ int s_hist[64], s_ban[64], s_nban;
   __shared__ unsigned char s_flag[kBeamChunk];  // bit 0: repetition penalty, bit 1: banned
-  __shared__ float s_wv[4][kMaxK];
-  __shared__ int s_wi[4][kMaxK];
+  __shared__ float s_wv[4 * K];
+  __shared__ int s_wi[4 * K];
   const int r = blockIdx.y, c = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (st.stopped[0]) return;
-  const int K = 2 * nb;
   const int n0 = c * kBeamChunk, n1 = min(n0 + kBeamChunk, V);
 
   // log_softmax statistics of the row: merge the lm_head workgroups' (max, sum) partials
@@ -106,70 +106,80 @@ __global__ __launch_bounds__(256) void vcap_beam_cand_kernel(BeamState st, const
   __syncthreads();
   const float run = st.run_score[r];
   // this thread's columns -> its own top-K (descending, ties: smaller token first)
-  float tv[kMaxK];
-  int ti[kMaxK];
+  constexpr int PER = kBeamChunk / 256;   // columns per thread
+  float cv[PER];
+  int ci[PER];
+  bool taken[PER];
 #pragma unroll
-  for (int k = 0; k < kMaxK; ++k) {
-    tv[k] = -INFINITY;
-    ti[k] = 0x7fffffff;
-  }
-  for (int n = n0 + tid; n < n1; n += 256) {
-    float lp = (logits[(long)r * V + n] - mx) - logsum;   // torch log_softmax: (x - max) - log(sum)
-    const int f = s_flag[n - n0];
-    if (f & 1) lp = lp < 0.f ? lp * rep : lp / rep;
-    if (f & 2) lp = -INFINITY;
-    if (n == eos && cur < min_new) lp = -INFINITY;
-    const float v = lp + run;
-    if (beats(v, n, tv[K - 1], ti[K - 1])) {
-      int k = K - 1;
-      while (k > 0 && beats(v, n, tv[k - 1], ti[k - 1])) {
-        tv[k] = tv[k - 1];
-        ti[k] = ti[k - 1];
-        --k;
-      }
-      tv[k] = v;
-      ti[k] = n;
+  for (int q = 0; q < PER; ++q) {
+    const int n = n0 + tid + q * 256;
+    taken[q] = n >= n1;
+    cv[q] = -INFINITY;
+    ci[q] = 0x7fffffff;
+    if (n < n1) {
+      float lp = (logits[(long)r * V + n] - mx) - logsum;   // torch log_softmax: (x - max) - log(sum)
+      const int f = s_flag[n - n0];
+      if (f & 1) lp = lp < 0.f ? lp * rep : lp / rep;
+      if (f & 2) lp = -INFINITY;
+      if (n == eos && cur < min_new) lp = -INFINITY;
+      cv[q] = lp + run;
+      ci[q] = n;
     }
   }
-  // block top-K: K rounds of (wave argmax of list heads, then across the 4 waves)
-  int head = 0;
+  // top-K of each wave (K rounds of wave argmax, no barrier), then of the 4 waves' 4K (wave 0)
+#pragma unroll
   for (int k = 0; k < K; ++k) {
-    float bv = head < K ? tv[head] : -INFINITY;
-    int bi = head < K ? ti[head] : 0x7fffffff;
-    // argmax_take breaks ties toward the smaller index, the list order
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+      if (!taken[q]) argmax_take(bv, bi, cv[q], ci[q]);   // ties: the smaller token
     wave_argmax(bv, bi);
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+      if (!taken[q] && ci[q] == bi) taken[q] = true;
     if (lane == 0) {
-      s_wv[wave][k] = bv;
-      s_wi[wave][k] = bi;
+      s_wv[wave * K + k] = bv;
+      s_wi[wave * K + k] = bi;
     }
-    __syncthreads();
-    float gv = s_wv[0][k];
-    int gi = s_wi[0][k];
-    for (int w = 1; w < 4; ++w) argmax_take(gv, gi, s_wv[w][k], s_wi[w][k]);
-    if (head < K && ti[head] == gi && tv[head] == gv) ++head;   // token ids are unique per row
-    if (tid == 0) {
-      st.cand_val[((long)r * gridDim.x + c) * K + k] = gv;
-      st.cand_tok[((long)r * gridDim.x + c) * K + k] = gi;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const bool have = lane < 4 * K;
+    float v = have ? s_wv[lane] : -INFINITY;
+    int i = have ? s_wi[lane] : 0x7fffffff;
+    bool gone = !have;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float bv = gone ? -INFINITY : v;
+      int bi = gone ? 0x7fffffff : i;
+      wave_argmax(bv, bi);
+      if (!gone && i == bi && v == bv) gone = true;
+      if (lane == 0) {
+        st.cand_val[((long)r * gridDim.x + c) * K + k] = bv;
+        st.cand_tok[((long)r * gridDim.x + c) * K + k] = bi;
+      }
     }
-    __syncthreads();
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // One workgroup, wave b = batch b.  Restates search.py beam_search (itself token-identical to the
 // reference's HF beam search, tests/test_gpu_search.py) for one step `cur`.
-__global__ __launch_bounds__(1024) void vcap_beam_select_kernel(BeamState st, int B, int nb, int L, int V, int C,
+template <int NB>
+__global__ __launch_bounds__(1024) void vcap_beam_select_kernel(BeamState st, int B, int L, int V, int C,
                                                                 int cur, int eos, float lpen, int S0, int anc_ld) {
+  constexpr int nb = NB;
   __shared__ int s_unsat[16], s_allhits[16];
   __shared__ int s_src[16][8];   // per batch: source beam of each new running beam
   __shared__ int s_anc[16 * 8][72];
   const int lane = threadIdx.x & 63, b = threadIdx.x >> 6;
   if (st.stopped[0]) return;   // HF's loop has ended: no further updates (uniform)
-  const int K = 2 * nb;
+  constexpr int K = 2 * NB;
   const bool live = b < B;
   // ---- top-2nb over the nb beams' chunk candidates (flat index beam * V + token, HF topk order)
-  float topv[kMaxK];
-  int topf[kMaxK];
+  float topv[K];
+  int topf[K];
   if (live) {
     const int ncand = nb * C * K;
     float cv[20];
@@ -191,6 +201,7 @@ __global__ __launch_bounds__(1024) void vcap_beam_select_kernel(BeamState st, in
         taken[q] = false;
       }
     }
+#pragma unroll
     for (int k = 0; k < K; ++k) {
       float bv = -INFINITY;
       int bi = 0x7fffffff;
@@ -208,8 +219,9 @@ __global__ __launch_bounds__(1024) void vcap_beam_select_kernel(BeamState st, in
   // ---- HF bookkeeping (wave-uniform scalar work; lanes split the per-position copies)
   int hits_all = 1;
   if (live) {
-    int src_beam[kMaxK], tok[kMaxK], hit[kMaxK];
-    float run_lp[kMaxK];
+    int src_beam[K], tok[K], hit[K];
+    float run_lp[K];
+#pragma unroll
     for (int k = 0; k < K; ++k) {
       src_beam[k] = topf[k] / V;
       tok[k] = topf[k] - src_beam[k] * V;
@@ -218,21 +230,41 @@ __global__ __launch_bounds__(1024) void vcap_beam_select_kernel(BeamState st, in
       hits_all &= hit[k];
     }
     // running beams for the next step: top-nb of run_lp (ties: lower candidate position)
-    int nxt[8];
+    // (indices select through unrolled compares: no dynamically indexed private arrays)
+    int nxt[NB];
+    float nxt_lp[NB];
+    int nxt_tok[NB], nxt_src[NB];
     {
       unsigned used = 0;
-      for (int i = 0; i < nb; ++i) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
         int best = -1;
+        float bv = 0.f;
+#pragma unroll
         for (int k = 0; k < K; ++k)
-          if (!(used >> k & 1) && (best < 0 || run_lp[k] > run_lp[best])) best = k;
+          if (!(used >> k & 1) && (best < 0 || run_lp[k] > bv)) {
+            best = k;
+            bv = run_lp[k];
+          }
         used |= 1u << best;
         nxt[i] = best;
+        nxt_lp[i] = bv;
+        int t = 0, sb = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (k == best) {
+            t = tok[k];
+            sb = src_beam[k];
+          }
+        nxt_tok[i] = t;
+        nxt_src[i] = sb;
       }
     }
     // finished-hypothesis candidates: score / (cur + 1)^length_penalty, masked as HF masks them
-    float sc[kMaxK];
+    float sc[K];
     const float denom = powf((float)(cur + 1), lpen);
     const int unsat = st.unsat[b];
+#pragma unroll
     for (int k = 0; k < K; ++k) {
       const bool did = hit[k] && k < nb;
       float v = topv[k] / denom;
@@ -242,60 +274,77 @@ __global__ __launch_bounds__(1024) void vcap_beam_select_kernel(BeamState st, in
       sc[k] = v;
     }
     // merge: [existing finished nb] ++ [2nb candidates] -> top-nb (ties: lower position)
-    float msc[24];
-    for (int i = 0; i < nb; ++i) msc[i] = st.beam_score[b * nb + i];
+    float msc[NB + K];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) msc[i] = st.beam_score[b * nb + i];
+#pragma unroll
     for (int k = 0; k < K; ++k) msc[nb + k] = sc[k];
-    int sel[8];
+    int sel[NB];
+    float sel_sc[NB];
     {
       unsigned used = 0;
-      for (int i = 0; i < nb; ++i) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
         int best = -1;
-        for (int k = 0; k < nb + K; ++k)
-          if (!(used >> k & 1) && (best < 0 || msc[k] > msc[best])) best = k;
+        float bv = 0.f;
+#pragma unroll
+        for (int k = 0; k < NB + K; ++k)
+          if (!(used >> k & 1) && (best < 0 || msc[k] > bv)) {
+            best = k;
+            bv = msc[k];
+          }
         used |= 1u << best;
         sel[i] = best;
+        sel_sc[i] = bv;
       }
     }
     // new finished set: gather rows (old finished entries, or a candidate = its source running
     // row + this step's token / beam index).  Read everything, then write (lanes = positions).
     const long base = (long)b * nb * L;
-    int new_seq[8], new_bidx[8];
     const int p = lane;   // lane = position (L <= 64)
-    for (int i = 0; i < nb; ++i) {
+    int new_seq[NB], new_bidx[NB], new_fin[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
       const int e = sel[i];
+      // the selected candidate's source row, token and hit flag (unrolled select)
+      int ctok = 0, csrc = 0, chit = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (e == NB + k) {
+          ctok = tok[k];
+          csrc = src_beam[k];
+          chit = hit[k] && k < NB;
+        }
       new_seq[i] = eos;
       new_bidx[i] = -1;
       if (p < L) {
-        if (e < nb) {
+        if (e < NB) {
           new_seq[i] = st.seqs[base + (long)e * L + p];
           new_bidx[i] = st.beam_idx[base + (long)e * L + p];
         } else {
-          const int k = e - nb;
-          new_seq[i] = p == cur ? tok[k] : st.run_seq[base + (long)src_beam[k] * L + p];
-          new_bidx[i] = p == cur ? b * nb + src_beam[k] : st.run_bidx[base + (long)src_beam[k] * L + p];
+          new_seq[i] = p == cur ? ctok : st.run_seq[base + (long)csrc * L + p];
+          new_bidx[i] = p == cur ? b * nb + csrc : st.run_bidx[base + (long)csrc * L + p];
         }
       }
+      new_fin[i] = e < NB ? st.fin[b * nb + e] : chit;
     }
-    float new_bscore[8];
-    int new_fin[8];
-    for (int i = 0; i < nb; ++i) {
-      const int e = sel[i];
-      new_bscore[i] = msc[e];
-      new_fin[i] = e < nb ? st.fin[b * nb + e] : (hit[e - nb] && (e - nb) < nb);
-    }
+    float new_bscore[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) new_bscore[i] = sel_sc[i];
     // new running set
-    int nr_seq[8], nr_bidx[8];
-    for (int i = 0; i < nb; ++i) {
-      const int k = nxt[i];
+    int nr_seq[NB], nr_bidx[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
       nr_seq[i] = eos;
       nr_bidx[i] = -1;
       if (p < L) {
-        nr_seq[i] = p == cur ? tok[k] : st.run_seq[base + (long)src_beam[k] * L + p];
-        nr_bidx[i] = p == cur ? b * nb + src_beam[k] : st.run_bidx[base + (long)src_beam[k] * L + p];
+        nr_seq[i] = p == cur ? nxt_tok[i] : st.run_seq[base + (long)nxt_src[i] * L + p];
+        nr_bidx[i] = p == cur ? b * nb + nxt_src[i] : st.run_bidx[base + (long)nxt_src[i] * L + p];
       }
     }
     __builtin_amdgcn_wave_barrier();
-    for (int i = 0; i < nb; ++i) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
       if (lane < L) {
         st.seqs[base + (long)i * L + lane] = new_seq[i];
         st.beam_idx[base + (long)i * L + lane] = new_bidx[i];
@@ -304,20 +353,23 @@ __global__ __launch_bounds__(1024) void vcap_beam_select_kernel(BeamState st, in
       }
     }
     if (lane == 0) {
-      for (int i = 0; i < nb; ++i) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
         st.beam_score[b * nb + i] = new_bscore[i];
         st.fin[b * nb + i] = new_fin[i];
-        st.run_score[b * nb + i] = run_lp[nxt[i]];
-        st.tok_next[b * nb + i] = tok[nxt[i]];
-        s_src[b][i] = src_beam[nxt[i]];
+        st.run_score[b * nb + i] = nxt_lp[i];
+        st.tok_next[b * nb + i] = nxt_tok[i];
+        s_src[b][i] = nxt_src[i];
       }
       // unsat update (cur + 1 generated tokens): best running vs worst finished
       const float best_len = powf((float)(cur + 1), lpen);
-      const float best_running = run_lp[nxt[0]] / best_len;
+      const float best_running = nxt_lp[0] / best_len;
       float mn = new_bscore[0];
-      for (int i = 1; i < nb; ++i) mn = fminf(mn, new_bscore[i]);
+#pragma unroll
+      for (int i = 1; i < NB; ++i) mn = fminf(mn, new_bscore[i]);
       bool any = false;
-      for (int i = 0; i < nb; ++i) any |= best_running > (new_fin[i] ? mn : kNeg);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) any |= best_running > (new_fin[i] ? mn : kNeg);
       const int u = unsat && any;
       st.unsat[b] = u;
       s_unsat[b] = u;
@@ -466,18 +518,31 @@ hipError_t vcap_beam_cand_dispatch(const BeamState& st, const float* logits, con
                                    const float* part_sum, int nblk, int rows, int V, int nb, int L, int cur,
                                    float rep, int ngram, int min_new, int eos, int chunks, hipStream_t s) {
   if (2 * nb > kMaxK || cur > 64 || chunks != vcap_beam_chunks(V)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(vcap_beam_cand_kernel, dim3(chunks, rows), dim3(256), 0, s, st, logits, part_max, part_sum,
-                     nblk, V, nb, L, cur, rep, ngram, min_new, eos);
-  return hipGetLastError();
+  const dim3 grid(chunks, rows);
+#define VCAP_CAND(NB)                                                                                          \
+  if (nb == NB) {                                                                                              \
+    hipLaunchKernelGGL((vcap_beam_cand_kernel<2 * NB>), grid, dim3(256), 0, s, st, logits, part_max, part_sum, \
+                       nblk, V, nb, L, cur, rep, ngram, min_new, eos);                                         \
+    return hipGetLastError();                                                                                  \
+  }
+  VCAP_CAND(2) VCAP_CAND(3) VCAP_CAND(4) VCAP_CAND(5) VCAP_CAND(6) VCAP_CAND(7) VCAP_CAND(8)
+#undef VCAP_CAND
+  return hipErrorInvalidValue;
 }
 
 hipError_t vcap_beam_select_dispatch(const BeamState& st, int B, int nb, int L, int V, int chunks, int cur, int eos,
                                      float length_penalty, int S0, int anc_ld, hipStream_t s) {
   if (B > 16 || nb > 8 || 2 * nb > kMaxK || L > 64 || anc_ld > 72 || nb * chunks * 2 * nb > 20 * 64)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(vcap_beam_select_kernel, dim3(1), dim3(64 * B), 0, s, st, B, nb, L, V, chunks, cur, eos,
-                     length_penalty, S0, anc_ld);
-  return hipGetLastError();
+#define VCAP_SEL(NB)                                                                                       \
+  if (nb == NB) {                                                                                          \
+    hipLaunchKernelGGL((vcap_beam_select_kernel<NB>), dim3(1), dim3(64 * B), 0, s, st, B, L, V, chunks, cur, \
+                       eos, length_penalty, S0, anc_ld);                                                   \
+    return hipGetLastError();                                                                              \
+  }
+  VCAP_SEL(2) VCAP_SEL(3) VCAP_SEL(4) VCAP_SEL(5) VCAP_SEL(6) VCAP_SEL(7) VCAP_SEL(8)
+#undef VCAP_SEL
+  return hipErrorInvalidValue;
 }
 
 hipError_t vcap_beam_output_dispatch(const BeamState& st, int B, int nb, int L, int* out_ids, int* out_len,

@@ -715,7 +715,7 @@ constexpr bool gemv_nsl_ok(int nsl) {
 template <typename T, int MT, int NTB, int PRO, int NSL>
 constexpr bool gemv_fits() {
   constexpr int KS = 4 * Frag<T>::kElems;
-  return gemv_nsl_ok<T>(NSL) && NSL * (NTB + (PRO == PRO_DIRECT ? MT : 0)) <= 48 &&
+  return gemv_nsl_ok<T>(NSL) && NSL * (NTB + (PRO == PRO_DIRECT ? MT : 0)) <= 64 &&
          (PRO != PRO_LN || NSL * KS * 4 <= 1024);
 }
 

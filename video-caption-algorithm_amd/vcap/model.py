@@ -203,6 +203,8 @@ class GenConfig:
     pad_token_id: int = 50256
     use_graph: bool = True
     max_blocks: int = 0      # >0: narrower decode grids (decode sharing the GPU with an encode)
+    num_beams: int = 1       # >1: device beam search (vcap_gpt2_beam_search, presets precise / detailed)
+    length_penalty: float = 1.0
 
     @classmethod
     def raw_greedy(cls, max_new_tokens: int = 24, eos: int = 50256, use_graph: bool = True) -> "GenConfig":
@@ -276,11 +278,16 @@ class HipGPT2Decoder:
 
     def generate_ids(self, prefix: torch.Tensor, prompt_ids: Sequence[int], cfg: GenConfig,
                      out: Optional[torch.Tensor] = None, logits_out: Optional[torch.Tensor] = None,
-                     workspace: Optional["_Workspace"] = None) -> torch.Tensor:
+                     workspace: Optional["_Workspace"] = None, lengths_out: Optional[torch.Tensor] = None
+                     ) -> torch.Tensor:
         """prefix [B,P,E] f32 device, prompt ids (BOS-only prompt = [eos]) -> int32 [B, max_new] EOS-padded.
 
         `workspace` (KV pages + decode scratch) defaults to the decoder's own; concurrent decodes on
-        different streams pass one each (the captured graph is keyed on it)."""
+        different streams pass one each (the captured graph is keyed on it).  cfg.num_beams > 1 runs
+        the device beam search instead of greedy; `lengths_out` (int32 [B]) then receives each best
+        hypothesis' length (HF returns the first max(lengths) columns)."""
+        if cfg.num_beams > 1:
+            return self._beam_ids(prefix, prompt_ids, cfg, out, workspace, lengths_out)
         B, P, E = prefix.shape
         if P != self.prefix_len or E != self.arch.n_embd:
             raise ValueError(f"prefix shape {tuple(prefix.shape)} != [B,{self.prefix_len},{self.arch.n_embd}]")
@@ -314,6 +321,32 @@ class HipGPT2Decoder:
         N.check(N.lib().vcap_gpt2_generate(C.byref(self.desc), C.byref(gp), prefix.data_ptr(), arr, len(ids), B,
                                            out.data_ptr(), N.ptr(logits_out), ws.data_ptr(), ws.numel(),
                                            _stream(prefix.device)), "vcap_gpt2_generate")
+        return out
+
+
+    def _beam_ids(self, prefix, prompt_ids, cfg: GenConfig, out, workspace, lengths_out):
+        B, P, E = prefix.shape
+        if P != self.prefix_len or E != self.arch.n_embd:
+            raise ValueError(f"prefix shape {tuple(prefix.shape)} != [B,{self.prefix_len},{self.arch.n_embd}]")
+        ids = [int(i) for i in prompt_ids]
+        mx = int(cfg.max_new_tokens)
+        prefix = prefix.to(torch.float32).contiguous()
+        out = out if out is not None else torch.empty(B, mx, dtype=torch.int32, device=prefix.device)
+        if lengths_out is None:
+            lengths_out = torch.empty(B, dtype=torch.int32, device=prefix.device)
+        S0 = self.prefix_len + len(ids)
+        nbytes = int(N.lib().vcap_gpt2_beam_search_workspace_bytes(C.byref(self.desc), B, int(cfg.num_beams), S0, mx))
+        if nbytes == 0:
+            raise ValueError("vcap_gpt2_beam_search_workspace_bytes: unsupported shape")
+        ws = (workspace or self.ws).get(nbytes)
+        bp = N.BeamParams(num_beams=int(cfg.num_beams), max_new_tokens=mx, min_new_tokens=int(cfg.min_new_tokens),
+                          no_repeat_ngram_size=int(cfg.no_repeat_ngram_size),
+                          repetition_penalty=float(cfg.repetition_penalty), length_penalty=float(cfg.length_penalty),
+                          early_stopping=0, eos_token_id=int(cfg.eos_token_id), use_graph=int(bool(cfg.use_graph)))
+        arr = (C.c_int * max(len(ids), 1))(*ids)
+        N.check(N.lib().vcap_gpt2_beam_search(C.byref(self.desc), C.byref(bp), prefix.data_ptr(), arr, len(ids), B,
+                                              out.data_ptr(), lengths_out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                              _stream(prefix.device)), "vcap_gpt2_beam_search")
         return out
 
 

@@ -60,39 +60,26 @@ class _StepState:
 def beam_search_device(dec, prefix: torch.Tensor, prompt_ids: Sequence[int], *, num_beams: int, max_new_tokens: int,
                        min_new_tokens: int = 8, no_repeat_ngram_size: int = 3, repetition_penalty: float = 1.1,
                        eos: int = 50256, length_penalty: float = 1.0, use_graph: bool = True) -> List[List[int]]:
-    """The same search as `beam_search`, entirely on the device (vcap_gpt2_beam_search: fused
-    log_softmax / processor / top-2k kernels and a device bookkeeping kernel, one hipGraph, one
-    device->host copy of the result).  Persistent per-shape buffers keep the captured graph."""
+    """The same search as `beam_search`, entirely on the device (vcap_gpt2_beam_search through
+    HipGPT2Decoder.generate_ids: fused log_softmax / processor / top-2k kernels and a device
+    bookkeeping kernel, one hipGraph, one device->host copy of the result).  Persistent
+    per-shape prefix / output buffers keep the captured graph across calls."""
+    from .model import GenConfig
     B, P, E = prefix.shape
-    dev = prefix.device
-    ids = [int(i) for i in prompt_ids]
-    S0 = dec.prefix_len + len(ids)
     cache = dec.__dict__.setdefault("_beam_bufs", {})   # persistent per decoder and shape
-    key = (B, P, E, num_beams, max_new_tokens)
+    key = (B, num_beams, max_new_tokens)
     if key not in cache:
-        nbytes = int(N.lib().vcap_gpt2_beam_search_workspace_bytes(C.byref(dec.desc), B, num_beams, S0, max_new_tokens))
-        if nbytes == 0:
-            raise ValueError("vcap_gpt2_beam_search_workspace_bytes: unsupported shape")
-        cache[key] = {"pre": torch.empty(B, P, E, dtype=torch.float32, device=dev),
-                           "ids": torch.empty(B, max_new_tokens, dtype=torch.int32, device=dev),
-                           "len": torch.empty(B, dtype=torch.int32, device=dev), "ws": {}}
-    bufs = cache[key]
-    nbytes = int(N.lib().vcap_gpt2_beam_search_workspace_bytes(C.byref(dec.desc), B, num_beams, S0, max_new_tokens))
-    ws = bufs["ws"].get(S0)
-    if ws is None or ws.numel() < nbytes:
-        ws = bufs["ws"][S0] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    bufs["pre"].copy_(prefix)
-    bp = N.BeamParams(num_beams=int(num_beams), max_new_tokens=int(max_new_tokens),
-                      min_new_tokens=int(min_new_tokens), no_repeat_ngram_size=int(no_repeat_ngram_size),
-                      repetition_penalty=float(repetition_penalty), length_penalty=float(length_penalty),
-                      early_stopping=0, eos_token_id=int(eos), use_graph=int(bool(use_graph)))
-    arr = (C.c_int * max(len(ids), 1))(*ids)
-    N.check(N.lib().vcap_gpt2_beam_search(C.byref(dec.desc), C.byref(bp), bufs["pre"].data_ptr(), arr, len(ids), B,
-                                          bufs["ids"].data_ptr(), bufs["len"].data_ptr(), ws.data_ptr(), ws.numel(),
-                                          torch.cuda.current_stream(dev).cuda_stream), "vcap_gpt2_beam_search")
-    out = bufs["ids"].cpu()
-    n = int(bufs["len"].max().item())
-    return [list(map(int, r)) for r in out[:, :n].tolist()]
+        cache[key] = (torch.empty(B, P, E, dtype=torch.float32, device=prefix.device),
+                      torch.empty(B, max_new_tokens, dtype=torch.int32, device=prefix.device),
+                      torch.empty(B, dtype=torch.int32, device=prefix.device))
+    pre, out, lens = cache[key]
+    pre.copy_(prefix)
+    cfg = GenConfig(max_new_tokens, min_new_tokens, no_repeat_ngram_size, repetition_penalty, eos, eos, use_graph,
+                    num_beams=num_beams, length_penalty=length_penalty)
+    dec.generate_ids(pre, prompt_ids, cfg, out=out, lengths_out=lens)
+    ids = out.cpu()
+    n = int(lens.max().item())
+    return [list(map(int, r)) for r in ids[:, :n].tolist()]
 
 
 def _processors(scores: torch.Tensor, seqs: torch.Tensor, rep: float, ngram: int, min_new: int, eos: int):

@@ -118,7 +118,8 @@ class InferenceEngine:
                 s0 = c.prefix_len + len(tok.encode_prompt(prompt or ""))
             except ValueError:
                 s0 = c.prefix_len + 1   # an untokenizable prompt fails per request anyway
-            rows = min(rows, limit // s0, limit // max(1, preset_to_kwargs(preset).get("num_beams", 1)))
+            beams = max(1, preset_to_kwargs(preset).get("num_beams", 1))
+            rows = min(rows, limit // s0, limit // beams, 8 if beams > 1 else limit)  # device beam: B <= 8
         return max(1, rows)
 
     @torch.no_grad()

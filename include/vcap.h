@@ -215,7 +215,8 @@ int vcap_decode_attention(int dtype, const void* q, const void* k_pool, const vo
  *      MinNewTokens -> + beam scores -> top-2*num_beams, length_penalty, early_stopping=False).
  *      The whole search (prefill + max_new steps + bookkeeping) is one call, replayed as one
  *      hipGraph; out_ids [B, max_new] = each sequence's best finished hypothesis (EOS-padded),
- *      out_len [B] = its generated length (HF returns the first max(out_len) columns). ---- */
+ *      out_len [B] = its generated length (HF returns the first max(out_len) columns).
+ *      Limits: B <= 8 sequences, 2 <= num_beams <= 8, max_new <= 64, prefix+prompt+max_new <= 128. ---- */
 typedef struct vcap_beam_params {
   int num_beams;
   int max_new_tokens;

@@ -55,58 +55,73 @@ __global__ void vcap_beam_init_kernel(BeamState st, int B, int nb, int L, int S0
 
 // ---------------------------------------------------------------------------------------------
 // Candidates of one (row, vocab chunk): processed log-prob + running score, top-2nb of the chunk.
+// Every global load (the chunk's logits, the row's log_softmax partials, its history) is issued at
+// kernel start: one memory round trip, then LDS / register work.
 template <int K>
 __global__ __launch_bounds__(256) void vcap_beam_cand_kernel(BeamState st, const float* __restrict__ logits,
                                                              const float* __restrict__ part_max,
                                                              const float* __restrict__ part_sum, int nblk, int V,
                                                              int nb, int L, int cur, float rep, int ngram, int min_new,
                                                              int eos) {
+  constexpr int PER = kBeamChunk / 256;   // columns per thread
+  constexpr int PP = 4;                   // log_softmax partials per thread (nblk <= 1024)
   __shared__ float s_red[8];
   __shared__ int s_hist[64], s_ban[64], s_nban;
-  __shared__ unsigned char s_flag[kBeamChunk];  // bit 0: repetition penalty, bit 1: banned
+  __shared__ __attribute__((aligned(16))) unsigned char s_flag[kBeamChunk];  // bit 0: repetition penalty, bit 1: banned
   __shared__ float s_wv[4 * K];
   __shared__ int s_wi[4 * K];
   const int r = blockIdx.y, c = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (st.stopped[0]) return;
   const int n0 = c * kBeamChunk, n1 = min(n0 + kBeamChunk, V);
-
-  // log_softmax statistics of the row: merge the lm_head workgroups' (max, sum) partials
-  float mx = -INFINITY;
-  for (int b = tid; b < nblk; b += 256) mx = fmaxf(mx, part_max[(long)r * nblk + b]);
+  // ---- loads
+  const int stopped = st.stopped[0];
+  float x[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int n = min(n0 + tid + q * 256, n1 - 1);
+    x[q] = logits[(long)r * V + n];
+  }
+  float pm[PP], ps[PP];
+#pragma unroll
+  for (int q = 0; q < PP; ++q) {
+    const int bb = tid + q * 256;
+    pm[q] = bb < nblk ? part_max[(long)r * nblk + bb] : -INFINITY;
+    ps[q] = bb < nblk ? part_sum[(long)r * nblk + bb] : 0.f;
+  }
+  const int hv = tid < cur ? st.run_seq[(long)r * L + tid] : 0;
+  const float run = st.run_score[r];
+  if (stopped) return;   // uniform
+  // ---- log_softmax statistics of the row (merge of the lm_head workgroups' (max, sum))
+  float mx = fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3]));
   mx = wave_max(mx);
   if (lane == 0) s_red[wave] = mx;
-  __syncthreads();
-  mx = fmaxf(fmaxf(s_red[0], s_red[1]), fmaxf(s_red[2], s_red[3]));
-  float sm = 0.f;
-  for (int b = tid; b < nblk; b += 256) sm += part_sum[(long)r * nblk + b] * expf(part_max[(long)r * nblk + b] - mx);
-  sm = wave_sum(sm);
-  __syncthreads();
-  if (lane == 0) s_red[4 + wave] = sm;
-  // row history (the running hypothesis of this row before this step) and its n-gram bans
-  if (tid < cur) s_hist[tid] = st.run_seq[(long)r * L + tid];
+  if (tid < cur) s_hist[tid] = hv;
   if (tid == 0) s_nban = 0;
   for (int i = tid; i < kBeamChunk; i += 256) s_flag[i] = 0;
   __syncthreads();
-  const float logsum = logf((s_red[4] + s_red[5]) + (s_red[6] + s_red[7]));
+  mx = fmaxf(fmaxf(s_red[0], s_red[1]), fmaxf(s_red[2], s_red[3]));
+  float sm = 0.f;
+#pragma unroll
+  for (int q = 0; q < PP; ++q) sm += ps[q] * expf(pm[q] - mx);
+  sm = wave_sum(sm);
+  if (lane == 0) s_red[4 + wave] = sm;
+  // n-gram bans of the row history
   if (ngram > 0 && cur >= ngram && tid + ngram <= cur) {
     bool match = true;
     for (int t = 0; t < ngram - 1; ++t) match &= s_hist[tid + t] == s_hist[cur - ngram + 1 + t];
     if (match) s_ban[atomicAdd(&s_nban, 1)] = s_hist[tid + ngram - 1];
   }
-  __syncthreads();
   if (rep != 1.0f && tid < cur) {
-    const unsigned o = (unsigned)(s_hist[tid] - n0);
+    const unsigned o = (unsigned)(hv - n0);
     if (o < (unsigned)(n1 - n0)) s_flag[o] = 1;   // duplicates write the same byte
   }
+  __syncthreads();
   if (tid < s_nban) {
     const unsigned o = (unsigned)(s_ban[tid] - n0);
-    if (o < (unsigned)(n1 - n0)) s_flag[o] |= 2;
+    if (o < (unsigned)(n1 - n0)) atomicOr((unsigned*)(s_flag + (o & ~3u)), 2u << (8 * (o & 3)));
   }
+  const float logsum = logf((s_red[4] + s_red[5]) + (s_red[6] + s_red[7]));
   __syncthreads();
-  const float run = st.run_score[r];
-  // this thread's columns -> its own top-K (descending, ties: smaller token first)
-  constexpr int PER = kBeamChunk / 256;   // columns per thread
   float cv[PER];
   int ci[PER];
   bool taken[PER];
@@ -114,17 +129,13 @@ __global__ __launch_bounds__(256) void vcap_beam_cand_kernel(BeamState st, const
   for (int q = 0; q < PER; ++q) {
     const int n = n0 + tid + q * 256;
     taken[q] = n >= n1;
-    cv[q] = -INFINITY;
-    ci[q] = 0x7fffffff;
-    if (n < n1) {
-      float lp = (logits[(long)r * V + n] - mx) - logsum;   // torch log_softmax: (x - max) - log(sum)
-      const int f = s_flag[n - n0];
-      if (f & 1) lp = lp < 0.f ? lp * rep : lp / rep;
-      if (f & 2) lp = -INFINITY;
-      if (n == eos && cur < min_new) lp = -INFINITY;
-      cv[q] = lp + run;
-      ci[q] = n;
-    }
+    float lp = (x[q] - mx) - logsum;   // torch log_softmax: (x - max) - log(sum)
+    const int f = n < n1 ? s_flag[n - n0] : 0;
+    if (f & 1) lp = lp < 0.f ? lp * rep : lp / rep;
+    if (f & 2) lp = -INFINITY;
+    if (n == eos && cur < min_new) lp = -INFINITY;
+    cv[q] = taken[q] ? -INFINITY : lp + run;
+    ci[q] = taken[q] ? 0x7fffffff : n;
   }
   // top-K of each wave (K rounds of wave argmax, no barrier), then of the 4 waves' 4K (wave 0)
 #pragma unroll
@@ -163,62 +174,92 @@ __global__ __launch_bounds__(256) void vcap_beam_cand_kernel(BeamState st, const
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// One workgroup, wave b = batch b.  Restates search.py beam_search (itself token-identical to the
-// reference's HF beam search, tests/test_gpu_search.py) for one step `cur`.
+// register "gather": a[idx] of a small unrolled array as an OR of masked terms (a compare /
+// select chain is canonicalised back into a dynamically indexed private array = scratch memory)
 template <int NB>
-__global__ __launch_bounds__(1024) void vcap_beam_select_kernel(BeamState st, int B, int L, int V, int C,
+VCAP_DEV int pick(const int (&a)[NB], int idx) {
+  int v = 0;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) v |= a[i] & -(int)(idx == i);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// One workgroup, wave b = batch b (B <= 8: 2 waves per SIMD, a 256-register budget).  Restates search.py beam_search (itself token-identical to the
+// reference's HF beam search, tests/test_gpu_search.py) for one step `cur`.  Lane p holds position
+// p (and p + 64 of the ancestry rows) of every beam of its batch; all state is loaded up front.
+template <int NB>
+__global__ __launch_bounds__(512) void vcap_beam_select_kernel(BeamState st, int B, int L, int V, int C,
                                                                 int cur, int eos, float lpen, int S0, int anc_ld) {
-  constexpr int nb = NB;
-  __shared__ int s_unsat[16], s_allhits[16];
-  __shared__ int s_src[16][8];   // per batch: source beam of each new running beam
-  __shared__ int s_anc[16 * 8][72];
-  const int lane = threadIdx.x & 63, b = threadIdx.x >> 6;
-  if (st.stopped[0]) return;   // HF's loop has ended: no further updates (uniform)
   constexpr int K = 2 * NB;
+  constexpr int NC = 20;   // candidates per lane (NB * C * K <= 1280)
+  __shared__ int s_unsat[8], s_allhits[8];
+  const int lane = threadIdx.x & 63, b = threadIdx.x >> 6;
   const bool live = b < B;
-  // ---- top-2nb over the nb beams' chunk candidates (flat index beam * V + token, HF topk order)
-  float topv[K];
-  int topf[K];
-  if (live) {
-    const int ncand = nb * C * K;
-    float cv[20];
-    int cf[20];
-    bool taken[20];
-    const int per = (ncand + 63) / 64;
+  const int p = lane;
+  const long base = (long)b * NB * L;
+  // ---- loads (one round trip)
+  const int stopped = st.stopped[0];
+  int rs[NB], rbx[NB], sq[NB], bix[NB], a0[NB], a1[NB], fn[NB];
+  float rsc[NB], bsc[NB];
+  float cv[NC];
+  int cf[NC];
+  int uns = 0;
 #pragma unroll
-    for (int q = 0; q < 20; ++q) {
-      const int i = lane + q * 64;
-      taken[q] = true;
-      cv[q] = -INFINITY;
-      cf[q] = 0x7fffffff;
-      if (q < per && i < ncand) {
-        const int beam = i / (C * K), rest = i % (C * K);
-        const long src = (long)(b * nb + beam) * C * K + rest;
-        const int t = st.cand_tok[src];
-        cv[q] = t < V ? st.cand_val[src] : -INFINITY;
-        cf[q] = t < V ? beam * V + t : 0x7fffffff;   // (a chunk with fewer than 2nb columns)
-        taken[q] = false;
-      }
-    }
+  for (int i = 0; i < NB; ++i) {
+    const bool pv = live && p < L;
+    rs[i] = pv ? st.run_seq[base + (long)i * L + p] : eos;
+    rbx[i] = pv ? st.run_bidx[base + (long)i * L + p] : -1;
+    sq[i] = pv ? st.seqs[base + (long)i * L + p] : eos;
+    bix[i] = pv ? st.beam_idx[base + (long)i * L + p] : -1;
+    const long ar = (long)(b * NB + i) * anc_ld;
+    a0[i] = live && p < anc_ld ? st.anc[ar + p] : 0;
+    a1[i] = live && p + 64 < anc_ld ? st.anc[ar + p + 64] : 0;
+    rsc[i] = live ? st.run_score[b * NB + i] : 0.f;
+    bsc[i] = live ? st.beam_score[b * NB + i] : 0.f;
+    fn[i] = live ? st.fin[b * NB + i] : 0;
+  }
+  if (live) uns = st.unsat[b];
+  const int ncand = NB * C * K;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      float bv = -INFINITY;
-      int bi = 0x7fffffff;
-#pragma unroll
-      for (int q = 0; q < 20; ++q)
-        if (!taken[q]) argmax_take(bv, bi, cv[q], cf[q]);
-      wave_argmax(bv, bi);
-#pragma unroll
-      for (int q = 0; q < 20; ++q)
-        if (!taken[q] && cf[q] == bi) taken[q] = true;
-      topv[k] = bv;
-      topf[k] = bi;
+  for (int q = 0; q < NC; ++q) {
+    const int i = lane + q * 64;
+    cv[q] = -INFINITY;
+    cf[q] = 0x7fffffff;
+    if (live && i < ncand) {
+      const int beam = i / (C * K), rest = i - beam * (C * K);
+      const long src = (long)(b * NB + beam) * C * K + rest;
+      const int t = st.cand_tok[src];
+      const float v = st.cand_val[src];
+      cv[q] = t < V ? v : -INFINITY;
+      cf[q] = t < V ? beam * V + t : 0x7fffffff;   // (a chunk with fewer than 2nb columns)
     }
   }
-  // ---- HF bookkeeping (wave-uniform scalar work; lanes split the per-position copies)
+  if (stopped) return;   // HF's loop has ended: no further updates (uniform)
   int hits_all = 1;
   if (live) {
+    // ---- top-2nb over the beams' chunk candidates (flat index beam * V + token, HF topk order)
+    float topv[K];
+    int topf[K];
+    {
+      bool taken[NC];
+#pragma unroll
+      for (int q = 0; q < NC; ++q) taken[q] = cf[q] == 0x7fffffff;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int q = 0; q < NC; ++q)
+          if (!taken[q]) argmax_take(bv, bi, cv[q], cf[q]);
+        wave_argmax(bv, bi);
+#pragma unroll
+        for (int q = 0; q < NC; ++q)
+          if (!taken[q] && cf[q] == bi) taken[q] = true;
+        topv[k] = bv;
+        topf[k] = bi;
+      }
+    }
     int src_beam[K], tok[K], hit[K];
     float run_lp[K];
 #pragma unroll
@@ -226,14 +267,12 @@ __global__ __launch_bounds__(1024) void vcap_beam_select_kernel(BeamState st, in
       src_beam[k] = topf[k] / V;
       tok[k] = topf[k] - src_beam[k] * V;
       hit[k] = (tok[k] == eos) || (cur + 1 >= L);
-      run_lp[k] = topv[k] + (hit[k] ? kNeg : -0.0f);
+      run_lp[k] = topv[k] + (hit[k] ? kNeg : -0.0f);   // topk_lp + hits * -1e9
       hits_all &= hit[k];
     }
     // running beams for the next step: top-nb of run_lp (ties: lower candidate position)
-    // (indices select through unrolled compares: no dynamically indexed private arrays)
-    int nxt[NB];
-    float nxt_lp[NB];
     int nxt_tok[NB], nxt_src[NB];
+    float nxt_lp[NB];
     {
       unsigned used = 0;
 #pragma unroll
@@ -247,147 +286,93 @@ __global__ __launch_bounds__(1024) void vcap_beam_select_kernel(BeamState st, in
             bv = run_lp[k];
           }
         used |= 1u << best;
-        nxt[i] = best;
         nxt_lp[i] = bv;
-        int t = 0, sb = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-          if (k == best) {
-            t = tok[k];
-            sb = src_beam[k];
-          }
-        nxt_tok[i] = t;
-        nxt_src[i] = sb;
+        nxt_tok[i] = pick<K>(tok, best);
+        nxt_src[i] = pick<K>(src_beam, best);
       }
     }
     // finished-hypothesis candidates: score / (cur + 1)^length_penalty, masked as HF masks them
-    float sc[K];
+    float msc[NB + K];
     const float denom = powf((float)(cur + 1), lpen);
-    const int unsat = st.unsat[b];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) msc[i] = bsc[i];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const bool did = hit[k] && k < nb;
+      const bool did = hit[k] && k < NB;
       float v = topv[k] / denom;
-      v = v + -0.0f;                        // full (early_stopping is False): + 0 * -1e9
-      v = v + (unsat ? -0.0f : kNeg);       // + (~unsat) * -1e9
-      v = v + (did ? -0.0f : kNeg);         // + (~did) * -1e9
-      sc[k] = v;
+      v = v + -0.0f;                     // full (early_stopping is False): + 0 * -1e9
+      v = v + (uns ? -0.0f : kNeg);      // + (~unsat) * -1e9
+      v = v + (did ? -0.0f : kNeg);      // + (~did) * -1e9
+      msc[NB + k] = v;
     }
-    // merge: [existing finished nb] ++ [2nb candidates] -> top-nb (ties: lower position)
-    float msc[NB + K];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) msc[i] = st.beam_score[b * nb + i];
-#pragma unroll
-    for (int k = 0; k < K; ++k) msc[nb + k] = sc[k];
-    int sel[NB];
-    float sel_sc[NB];
+    // merge [existing finished nb] ++ [2nb candidates] -> top-nb (ties: lower position)
+    int new_seq[NB], new_bidx[NB], new_fin[NB];
+    float new_bsc[NB];
     {
       unsigned used = 0;
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        int best = -1;
+        int e = -1;
         float bv = 0.f;
 #pragma unroll
         for (int k = 0; k < NB + K; ++k)
-          if (!(used >> k & 1) && (best < 0 || msc[k] > bv)) {
-            best = k;
+          if (!(used >> k & 1) && (e < 0 || msc[k] > bv)) {
+            e = k;
             bv = msc[k];
           }
-        used |= 1u << best;
-        sel[i] = best;
-        sel_sc[i] = bv;
-      }
-    }
-    // new finished set: gather rows (old finished entries, or a candidate = its source running
-    // row + this step's token / beam index).  Read everything, then write (lanes = positions).
-    const long base = (long)b * nb * L;
-    const int p = lane;   // lane = position (L <= 64)
-    int new_seq[NB], new_bidx[NB], new_fin[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int e = sel[i];
-      // the selected candidate's source row, token and hit flag (unrolled select)
-      int ctok = 0, csrc = 0, chit = 0;
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        if (e == NB + k) {
-          ctok = tok[k];
-          csrc = src_beam[k];
-          chit = hit[k] && k < NB;
-        }
-      new_seq[i] = eos;
-      new_bidx[i] = -1;
-      if (p < L) {
+        used |= 1u << e;
+        new_bsc[i] = bv;
         if (e < NB) {
-          new_seq[i] = st.seqs[base + (long)e * L + p];
-          new_bidx[i] = st.beam_idx[base + (long)e * L + p];
+          new_seq[i] = pick<NB>(sq, e);
+          new_bidx[i] = pick<NB>(bix, e);
+          new_fin[i] = pick<NB>(fn, e);
         } else {
-          new_seq[i] = p == cur ? ctok : st.run_seq[base + (long)csrc * L + p];
-          new_bidx[i] = p == cur ? b * nb + csrc : st.run_bidx[base + (long)csrc * L + p];
+          const int k = e - NB;
+          const int cs = pick<K>(src_beam, k);
+          new_seq[i] = p == cur ? pick<K>(tok, k) : pick<NB>(rs, cs);
+          new_bidx[i] = p == cur ? b * NB + cs : pick<NB>(rbx, cs);
+          new_fin[i] = pick<K>(hit, k) && k < NB;
         }
       }
-      new_fin[i] = e < NB ? st.fin[b * nb + e] : chit;
     }
-    float new_bscore[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) new_bscore[i] = sel_sc[i];
-    // new running set
-    int nr_seq[NB], nr_bidx[NB];
+    // ---- writes
+    const int pos = S0 + cur;   // the next forward writes this position (own physical row)
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      nr_seq[i] = eos;
-      nr_bidx[i] = -1;
+      const int src = nxt_src[i];
       if (p < L) {
-        nr_seq[i] = p == cur ? nxt_tok[i] : st.run_seq[base + (long)nxt_src[i] * L + p];
-        nr_bidx[i] = p == cur ? b * nb + nxt_src[i] : st.run_bidx[base + (long)nxt_src[i] * L + p];
+        st.seqs[base + (long)i * L + p] = new_seq[i];
+        st.beam_idx[base + (long)i * L + p] = new_bidx[i];
+        st.run_seq[base + (long)i * L + p] = p == cur ? nxt_tok[i] : pick<NB>(rs, src);
+        st.run_bidx[base + (long)i * L + p] = p == cur ? b * NB + src : pick<NB>(rbx, src);
       }
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      if (lane < L) {
-        st.seqs[base + (long)i * L + lane] = new_seq[i];
-        st.beam_idx[base + (long)i * L + lane] = new_bidx[i];
-        st.run_seq[base + (long)i * L + lane] = nr_seq[i];
-        st.run_bidx[base + (long)i * L + lane] = nr_bidx[i];
-      }
+      const long ar = (long)(b * NB + i) * anc_ld;
+      if (p < anc_ld) st.anc[ar + p] = p < pos ? pick<NB>(a0, src) : b * NB + i;
+      if (p + 64 < anc_ld) st.anc[ar + p + 64] = p + 64 < pos ? pick<NB>(a1, src) : b * NB + i;
     }
     if (lane == 0) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        st.beam_score[b * nb + i] = new_bscore[i];
-        st.fin[b * nb + i] = new_fin[i];
-        st.run_score[b * nb + i] = nxt_lp[i];
-        st.tok_next[b * nb + i] = nxt_tok[i];
-        s_src[b][i] = nxt_src[i];
+        st.beam_score[b * NB + i] = new_bsc[i];
+        st.fin[b * NB + i] = new_fin[i];
+        st.run_score[b * NB + i] = nxt_lp[i];
+        st.tok_next[b * NB + i] = nxt_tok[i];
       }
       // unsat update (cur + 1 generated tokens): best running vs worst finished
-      const float best_len = powf((float)(cur + 1), lpen);
-      const float best_running = nxt_lp[0] / best_len;
-      float mn = new_bscore[0];
+      const float best_running = nxt_lp[0] / powf((float)(cur + 1), lpen);
+      float mn = new_bsc[0];
 #pragma unroll
-      for (int i = 1; i < NB; ++i) mn = fminf(mn, new_bscore[i]);
+      for (int i = 1; i < NB; ++i) mn = fminf(mn, new_bsc[i]);
       bool any = false;
 #pragma unroll
       for (int i = 0; i < NB; ++i) any |= best_running > (new_fin[i] ? mn : kNeg);
-      const int u = unsat && any;
+      const int u = uns && any;
       st.unsat[b] = u;
       s_unsat[b] = u;
       s_allhits[b] = hits_all;
     }
   }
   __syncthreads();
-  // ---- K/V ancestry: row b*nb+i continues source row b*nb+src; position S0+cur is its own
-  const int pos = S0 + cur;   // the next forward writes this position
-  for (int idx = threadIdx.x; idx < B * nb * anc_ld; idx += blockDim.x) {
-    const int r = idx / anc_ld, p = idx % anc_ld;
-    s_anc[r][p] = st.anc[(long)(r / nb * nb + s_src[r / nb][r % nb]) * anc_ld + p];
-  }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < B * nb * anc_ld; idx += blockDim.x) {
-    const int r = idx / anc_ld, p = idx % anc_ld;
-    st.anc[(long)r * anc_ld + p] = p < pos ? s_anc[r][p] : r;
-  }
   if (threadIdx.x == 0) {
     int any_unsat = 0, all_hits = 1;
     for (int i = 0; i < B; ++i) {
@@ -517,7 +502,7 @@ hipError_t vcap_beam_init_dispatch(const BeamState& st, int B, int nb, int L, in
 hipError_t vcap_beam_cand_dispatch(const BeamState& st, const float* logits, const float* part_max,
                                    const float* part_sum, int nblk, int rows, int V, int nb, int L, int cur,
                                    float rep, int ngram, int min_new, int eos, int chunks, hipStream_t s) {
-  if (2 * nb > kMaxK || cur > 64 || chunks != vcap_beam_chunks(V)) return hipErrorInvalidValue;
+  if (2 * nb > kMaxK || cur > 64 || chunks != vcap_beam_chunks(V) || nblk > 1024) return hipErrorInvalidValue;
   const dim3 grid(chunks, rows);
 #define VCAP_CAND(NB)                                                                                          \
   if (nb == NB) {                                                                                              \
@@ -532,7 +517,7 @@ hipError_t vcap_beam_cand_dispatch(const BeamState& st, const float* logits, con
 
 hipError_t vcap_beam_select_dispatch(const BeamState& st, int B, int nb, int L, int V, int chunks, int cur, int eos,
                                      float length_penalty, int S0, int anc_ld, hipStream_t s) {
-  if (B > 16 || nb > 8 || 2 * nb > kMaxK || L > 64 || anc_ld > 72 || nb * chunks * 2 * nb > 20 * 64)
+  if (B > 8 || nb > 8 || 2 * nb > kMaxK || L > 64 || anc_ld > 128 || nb * chunks * 2 * nb > 20 * 64)
     return hipErrorInvalidValue;
 #define VCAP_SEL(NB)                                                                                       \
   if (nb == NB) {                                                                                          \

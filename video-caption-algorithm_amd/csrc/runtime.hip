@@ -1037,9 +1037,9 @@ int vcap_gpt2_beam_search(const vcap_gpt2_desc* d, const vcap_beam_params* bp, c
       (prompt_len && !prompt_ids))
     return fail(VCAP_E_ARG, "vcap_gpt2_beam_search: bad arguments");
   const int nb = bp->num_beams, L = bp->max_new_tokens, S0 = d->prefix_len + prompt_len;
-  if (nb < 2 || nb > 8 || B > 16 || L <= 0 || L > 64 || S0 + L > 72 || S0 + L > d->n_positions)
-    return fail(VCAP_E_UNSUPPORTED, "vcap_gpt2_beam_search: needs 2 <= num_beams <= 8, B <= 16, max_new <= 64, "
-                                    "prefix + prompt + max_new <= 72");
+  if (nb < 2 || nb > 8 || B > 8 || L <= 0 || L > 64 || S0 + L > 128 || S0 + L > d->n_positions)
+    return fail(VCAP_E_UNSUPPORTED, "vcap_gpt2_beam_search: needs 2 <= num_beams <= 8, B <= 8, max_new <= 64, "
+                                    "prefix + prompt + max_new <= 128");
   if (B * nb * S0 > kMaxDecodeRows) return fail(VCAP_E_UNSUPPORTED, "B*num_beams*(prefix+prompt) exceeds max rows");
   if (bp->early_stopping != 0) return fail(VCAP_E_UNSUPPORTED, "only early_stopping=False (the reference's presets)");
   if (nb * vcap_beam_chunks(d->vocab) * 2 * nb > 20 * 64)

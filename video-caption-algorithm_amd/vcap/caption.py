@@ -49,13 +49,20 @@ class _Identity:
 
 
 class _WTE:
-    """decoder.model.transformer.wte: embedding lookup of the packed (device) table."""
+    """decoder.model.transformer.wte: the token embedding as the reference's nn.Embedding returns it
+    (fp32 rows, core/scripts/benchmark_baseline.py:162-227 feeds them back as inputs_embeds).  The
+    decoder's own table may be bf16 (the throughput mode); the fp32 rows are uploaded on first use."""
 
-    def __init__(self, table: torch.Tensor):
+    def __init__(self, table: torch.Tensor, table_f32=None):
         self.weight = table
+        self._src = table_f32       # host fp32 [V, E] (state dict) or None: use `table` as is
+        self._f32 = None
 
     def __call__(self, ids: torch.Tensor) -> torch.Tensor:
-        return self.weight[ids.to(self.weight.device)].float()
+        if self._src is not None and self._f32 is None:
+            self._f32 = torch.from_numpy(np.ascontiguousarray(self._src, dtype=np.float32)).to(self.weight.device)
+        t = self._f32 if self._f32 is not None else self.weight
+        return t[ids.to(t.device)].float()
 
 
 class HipPast:
@@ -129,7 +136,7 @@ class HipTextDecoder:
         self.mapper_op = HipPrefix(sd, arch.n_embd, prefix_len, 0.0, 0.0, device)
         self.tokenizer = load_tokenizer(tokenizer_dir, arch.eos_token_id)
         self.use_graph = use_graph
-        self.model = HipGPT2LMHead(self.hip, arch, _WTE(self.hip.wte))
+        self.model = HipGPT2LMHead(self.hip, arch, _WTE(self.hip.wte, sd["decoder.model.transformer.wte.weight"]))
 
     def mapper(self, emb: torch.Tensor) -> torch.Tensor:
         """Linear 256 -> P*E on the HIP path (cupy_linear_mapper / CuPyLinearCompat replacement)."""

@@ -58,13 +58,13 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="no encode/decode overlap (each step's decode finishes before the next encode starts)")
-    ap.add_argument("--reserve-cus", type=int, default=32,
+    ap.add_argument("--reserve-cus", type=int, default=0,
                     help="CUs the encode stream leaves to the decode stream (CU-masked stream; 0 = none)")
-    ap.add_argument("--decode-blocks", type=int, default=128,
+    ap.add_argument("--decode-blocks", type=int, default=96,
                     help="cap the decode GEMV grids near this many workgroups (0 = whole-chip grids)")
     ap.add_argument("--dec-lanes", type=int, default=2,
                     help="decodes in flight at once (own stream + workspace + graph each)")
-    ap.add_argument("--dec-group", type=int, default=1,
+    ap.add_argument("--dec-group", type=int, default=2,
                     help="consecutive batches decoded together as one decode of group*batch rows")
     ap.add_argument("--confine-decode", action="store_true",
                     help="mask the decode streams to the reserved CUs (default: unmasked, high priority)")

@@ -49,3 +49,20 @@ def test_caption_sharded_two_ranks_match_goldens(tmp_path, name):
     assert res["world"] == 2 and got.shape[0] == meta["B"]
     assert np.array_equal(got[:, :exp.shape[1]], exp)
     assert (got[:, exp.shape[1]:] == eos).all()
+
+
+def test_bench_two_ranks_gloo(tmp_path):
+    """The N>1 bench path (torchrun, one process per rank, sharded videos, decode-lane id copies,
+    ONE end-of-run all-gather, MAX-over-ranks timing) rehearsed with 2 ranks sharing the box's
+    GPU over gloo (VCAP_BENCH_DIST_BACKEND): rank 0 prints one JSON line for n_gpus = 2."""
+    env = dict(os.environ, VCAP_BENCH_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(HERE.parent / "bench.py"), "--gpus", "2",
+           "--steps", "4", "--warmup", "2", "--cpu-baseline-s", "0", "--no-parity", "--no-decode-alone",
+           "--host-e2e", "0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=160)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["global_batch"] == 16

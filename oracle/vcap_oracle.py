@@ -25,7 +25,7 @@ A plain fp32 restatement (torch CPU tensors used as an array library) of:
 
 Parity pin: tests/golden/make_goldens.py runs the reference's own code
 (ViTFrameEncoder, InferenceEngine._generate_once, GPT2TextDecoder.generate)
-in the build container and records its outputs; tests/test_oracle_golden.py
+in the build container and records its outputs; tests/test_cpu_oracle.py
 checks this restatement against those fixtures.
 """
 from __future__ import annotations

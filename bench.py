@@ -384,13 +384,15 @@ def main():
                                    f"(BASELINE {workload_tag(args, world)})",
                        "num_beams": args.beams,
                        "vit": args.vit, "gpt2": args.gpt2, "batch_per_gpu": B, "global_batch": world * B,
-                       "frames": T, "max_new_tokens": args.max_new, "decode": args.decode,
+                       "frames": T, "max_new_tokens": args.max_new,
+                       "decode": args.decode if args.beams == 1 else f"beam-{args.beams} (device beam search, HF _beam_search)",
                        "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}",
                        "decode_block_cap": cfg.max_blocks,
                        "schedule": "serial" if args.serial else
                        f"CU-masked encode stream (off {args.reserve_cus} CUs) overlapped with {args.dec_lanes} decode "
                        f"lane(s) in flight; each decode = {args.dec_group} consecutive batch(es) as one "
-                       f"{args.dec_group * B}-row greedy decode graph",
+                       (f"{args.dec_group * B}-row greedy decode graph" if args.beams == 1 else
+                        f"{args.dec_group * B} x {args.beams}-beam search graph"),
                        "dec_lanes": 1 if args.serial else args.dec_lanes,
                        "dec_group": 1 if args.serial else args.dec_group},
             "value_definition": "pipelined throughput: videos captioned / wall time of the timed steps "

@@ -391,8 +391,8 @@ def main():
                        "schedule": "serial" if args.serial else
                        f"CU-masked encode stream (off {args.reserve_cus} CUs) overlapped with {args.dec_lanes} decode "
                        f"lane(s) in flight; each decode = {args.dec_group} consecutive batch(es) as one "
-                       (f"{args.dec_group * B}-row greedy decode graph" if args.beams == 1 else
-                        f"{args.dec_group * B} x {args.beams}-beam search graph"),
+                       + (f"{args.dec_group * B}-row greedy decode graph" if args.beams == 1 else
+                          f"{args.dec_group * B} x {args.beams}-beam search graph"),
                        "dec_lanes": 1 if args.serial else args.dec_lanes,
                        "dec_group": 1 if args.serial else args.dec_group},
             "value_definition": "pipelined throughput: videos captioned / wall time of the timed steps "

@@ -168,3 +168,15 @@ def test_caption_sharded_gloo(world, n):
         p.join(timeout=60)
     want = [[v * 10 + j for j in range(5)] for v in range(n)]
     assert all(res[r] == want for r in range(world))
+
+
+def test_driver_entry_scripts_compile_cleanly():
+    """bench.py / __graft_entry__.py are run by the driver on the GPU box: they must compile without
+    even a SyntaxWarning (an implicit string concatenation next to a parenthesised expression
+    compiles as a call and fails only at run time)."""
+    import warnings
+    root = Path(__file__).resolve().parents[1]
+    for name in ("bench.py", "__graft_entry__.py"):
+        with warnings.catch_warnings():
+            warnings.simplefilter("error")
+            compile((root / name).read_text(), name, "exec")

@@ -10,7 +10,8 @@ import torch  # noqa: E402
 
 from vcap import _native as N  # noqa: E402
 
-BT, NT, H = 128, 197, 12
+import os
+BT, NT, H = int(os.environ.get("BT", "128")), 197, 12
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 qkv = torch.randn(BT * NT, 3 * H * 64, generator=g, device=dev).to(torch.bfloat16)
@@ -31,3 +32,5 @@ for _ in range(7):
 ms = statistics.median(ts)
 fl = 4.0 * BT * H * NT * NT * 64
 print(f"attention BT={BT} N={NT} H={H}: {ms * 1e3:.1f} us  {fl / ms / 1e9:.1f} TF", flush=True)
+if os.environ.get("DUMP"):
+    torch.save(out.cpu(), os.environ["DUMP"])

@@ -122,33 +122,35 @@ __global__ __launch_bounds__(256) void vcap_beam_cand_kernel(BeamState st, const
   }
   const float logsum = logf((s_red[4] + s_red[5]) + (s_red[6] + s_red[7]));
   __syncthreads();
+  // taken / out-of-chunk entries hold (-inf, INT_MAX): they lose every comparison against a live
+  // entry (a live -inf keeps its token index), so the top-K rounds run branch-free
   float cv[PER];
   int ci[PER];
-  bool taken[PER];
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int n = n0 + tid + q * 256;
-    taken[q] = n >= n1;
     float lp = (x[q] - mx) - logsum;   // torch log_softmax: (x - max) - log(sum)
     const int f = n < n1 ? s_flag[n - n0] : 0;
     if (f & 1) lp = lp < 0.f ? lp * rep : lp / rep;
     if (f & 2) lp = -INFINITY;
     if (n == eos && cur < min_new) lp = -INFINITY;
-    cv[q] = taken[q] ? -INFINITY : lp + run;
-    ci[q] = taken[q] ? 0x7fffffff : n;
+    cv[q] = n < n1 ? lp + run : -INFINITY;
+    ci[q] = n < n1 ? n : 0x7fffffff;
   }
   // top-K of each wave (K rounds of wave argmax, no barrier), then of the 4 waves' 4K (wave 0)
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
+    float bv = cv[0];
+    int bi = ci[0];
 #pragma unroll
-    for (int q = 0; q < PER; ++q)
-      if (!taken[q]) argmax_take(bv, bi, cv[q], ci[q]);   // ties: the smaller token
+    for (int q = 1; q < PER; ++q) argmax_take(bv, bi, cv[q], ci[q]);   // ties: the smaller token
     wave_argmax(bv, bi);
 #pragma unroll
-    for (int q = 0; q < PER; ++q)
-      if (!taken[q] && ci[q] == bi) taken[q] = true;
+    for (int q = 0; q < PER; ++q) {
+      const bool hit = ci[q] == bi;
+      cv[q] = hit ? -INFINITY : cv[q];
+      ci[q] = hit ? 0x7fffffff : ci[q];
+    }
     if (lane == 0) {
       s_wv[wave * K + k] = bv;
       s_wi[wave * K + k] = bi;
@@ -159,13 +161,14 @@ __global__ __launch_bounds__(256) void vcap_beam_cand_kernel(BeamState st, const
     const bool have = lane < 4 * K;
     float v = have ? s_wv[lane] : -INFINITY;
     int i = have ? s_wi[lane] : 0x7fffffff;
-    bool gone = !have;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      float bv = gone ? -INFINITY : v;
-      int bi = gone ? 0x7fffffff : i;
+      float bv = v;
+      int bi = i;
       wave_argmax(bv, bi);
-      if (!gone && i == bi && v == bv) gone = true;
+      const bool hit = i == bi && v == bv;
+      v = hit ? -INFINITY : v;
+      i = hit ? 0x7fffffff : i;
       if (lane == 0) {
         st.cand_val[((long)r * gridDim.x + c) * K + k] = bv;
         st.cand_tok[((long)r * gridDim.x + c) * K + k] = bi;
@@ -198,41 +201,49 @@ __global__ __launch_bounds__(512) void vcap_beam_select_kernel(BeamState st, int
   const bool live = b < B;
   const int p = lane;
   const long base = (long)b * NB * L;
-  // ---- loads (one round trip)
+  // ---- loads (one round trip): every address clamped into range and every load unconditional
+  // (a guarded load is compiled as its own branch + wait: 57 serial round trips before this)
   const int stopped = st.stopped[0];
   int rs[NB], rbx[NB], sq[NB], bix[NB], a0[NB], a1[NB], fn[NB];
   float rsc[NB], bsc[NB];
   float cv[NC];
   int cf[NC];
-  int uns = 0;
+  const int bl = min(b, B - 1);
+  const long basel = (long)bl * NB * L;
+  const int pl = min(p, L - 1), pa0 = min(p, anc_ld - 1), pa1 = min(p + 64, anc_ld - 1);
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const bool pv = live && p < L;
-    rs[i] = pv ? st.run_seq[base + (long)i * L + p] : eos;
-    rbx[i] = pv ? st.run_bidx[base + (long)i * L + p] : -1;
-    sq[i] = pv ? st.seqs[base + (long)i * L + p] : eos;
-    bix[i] = pv ? st.beam_idx[base + (long)i * L + p] : -1;
-    const long ar = (long)(b * NB + i) * anc_ld;
-    a0[i] = live && p < anc_ld ? st.anc[ar + p] : 0;
-    a1[i] = live && p + 64 < anc_ld ? st.anc[ar + p + 64] : 0;
-    rsc[i] = live ? st.run_score[b * NB + i] : 0.f;
-    bsc[i] = live ? st.beam_score[b * NB + i] : 0.f;
-    fn[i] = live ? st.fin[b * NB + i] : 0;
+    rs[i] = st.run_seq[basel + (long)i * L + pl];
+    rbx[i] = st.run_bidx[basel + (long)i * L + pl];
+    sq[i] = st.seqs[basel + (long)i * L + pl];
+    bix[i] = st.beam_idx[basel + (long)i * L + pl];
+    const long ar = (long)(bl * NB + i) * anc_ld;
+    a0[i] = st.anc[ar + pa0];
+    a1[i] = st.anc[ar + pa1];
+    rsc[i] = st.run_score[bl * NB + i];
+    bsc[i] = st.beam_score[bl * NB + i];
+    fn[i] = st.fin[bl * NB + i];
   }
-  if (live) uns = st.unsat[b];
+  const int uns = st.unsat[bl];
   const int ncand = NB * C * K;
 #pragma unroll
   for (int q = 0; q < NC; ++q) {
-    const int i = lane + q * 64;
-    cv[q] = -INFINITY;
-    cf[q] = 0x7fffffff;
-    if (live && i < ncand) {
-      const int beam = i / (C * K), rest = i - beam * (C * K);
-      const long src = (long)(b * NB + beam) * C * K + rest;
-      const int t = st.cand_tok[src];
-      const float v = st.cand_val[src];
-      cv[q] = t < V ? v : -INFINITY;
-      cf[q] = t < V ? beam * V + t : 0x7fffffff;   // (a chunk with fewer than 2nb columns)
+    const int i = min(lane + q * 64, ncand - 1);
+    const int beam = i / (C * K), rest = i - beam * (C * K);
+    const long src = (long)(bl * NB + beam) * C * K + rest;
+    const int t = st.cand_tok[src];
+    const float v = st.cand_val[src];
+    const bool ok = lane + q * 64 < ncand && t < V;   // (a chunk with fewer than 2nb columns)
+    cv[q] = ok ? v : -INFINITY;
+    cf[q] = ok ? beam * V + t : 0x7fffffff;
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {   // positions past L read as HF's initial padding
+    if (p >= L) {
+      rs[i] = eos;
+      rbx[i] = -1;
+      sq[i] = eos;
+      bix[i] = -1;
     }
   }
   if (stopped) return;   // HF's loop has ended: no further updates (uniform)

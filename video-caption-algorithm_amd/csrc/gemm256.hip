@@ -76,6 +76,28 @@ VCAP_DEV u32x4 frag(const char* half, int row, int chunk) {
   return *reinterpret_cast<const u32x4*>(half + row * ROWB + ((chunk ^ (row & 7)) << 4));
 }
 
+// Output stores are streaming (nontemporal): a round's 128 KiB-per-CU write-back then does not
+// evict the A row panels / W tiles the next round re-reads from L2 (fc1 135.7 -> 127.5 us,
+// QKV 100 -> 97 us alone; profiles/r02_gemm_nt_store_ab.txt).
+template <typename V>
+VCAP_DEV void out_store(V* p, const V& v) {
+#ifdef VCAP_GEMM_PLAIN_STORE
+  *p = v;
+#else
+  __builtin_nontemporal_store(v, p);
+#endif
+}
+
+// read-once operand (the in-place residual)
+template <typename V>
+VCAP_DEV V once_load(const V* p) {
+#ifdef VCAP_NT_MORE
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 VCAP_DEV void lds_fence() { asm volatile("" ::: "memory"); }
 
 }  // namespace
@@ -347,8 +369,8 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
           transpose4_groups(x);
           const int ms = m0 + wr * 128 + qm * 64 + (i + (fg >> 1)) * 16 + fr;
           if (ms < M && nb < N)
-            *reinterpret_cast<u32x4*>((uint8_t*)C + (long)ms * ldc + nb + (fg & 1) * 16) =
-                (u32x4){x[0], x[1], x[2], x[3]};
+            out_store(reinterpret_cast<u32x4*>((uint8_t*)C + (long)ms * ldc + nb + (fg & 1) * 16),
+                      (u32x4){x[0], x[1], x[2], x[3]});
         }
       }
   } else if (sizeof(TOut) == 2 && (EPI == 0 || EPI == 1) && (N & 31) == 0 && (ldc & 7) == 0 &&
@@ -383,7 +405,7 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
           const uint32_t r0 = (uint32_t)xor16_i((int)(odd ? p[0][0] : p[1][0]));
           const uint32_t r1 = (uint32_t)xor16_i((int)(odd ? p[0][1] : p[1][1]));
           const u32x4 o = odd ? (u32x4){r0, r1, p[1][0], p[1][1]} : (u32x4){p[0][0], p[0][1], r0, r1};
-          if (m < M && nb < N) *reinterpret_cast<u32x4*>(C + (long)m * ldc + col) = o;
+          if (m < M && nb < N) out_store(reinterpret_cast<u32x4*>(C + (long)m * ldc + col), o);
         }
       }
   } else {
@@ -406,20 +428,20 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
           } else if constexpr (EPI == 2) {
-            v += *reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n);
+            v += once_load(reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n));
           } else if constexpr (EPI == 3) {
             if (epi.act == 1)
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
             orow = epi.G ? (long)(m / epi.G) * epi.Gs + epi.goff + (m % epi.G) : (long)m;
-            if (epi.res_mode == 1) v += *reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n);
+            if (epi.res_mode == 1) v += once_load(reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n));
             else if (epi.res_mode == 2)
               v += *reinterpret_cast<const f32x4*>(epi.res + (long)((m % epi.G) + epi.roff) * epi.ldr + n);
           }
           if constexpr (sizeof(TOut) == 2) {
-            *reinterpret_cast<u32x2*>(C + orow * ldc + n) = (u32x2){pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
+            out_store(reinterpret_cast<u32x2*>(C + orow * ldc + n), (u32x2){pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)});
           } else {
-            *reinterpret_cast<f32x4*>(C + orow * ldc + n) = v;
+            out_store(reinterpret_cast<f32x4*>(C + orow * ldc + n), v);
           }
         }
       }

@@ -21,11 +21,13 @@ VCAP_DEV bf16_t f2bf(float f) {
   return (bf16_t)(u >> 16);
 }
 
-// two f32 -> packed bf16x2 (round-to-nearest-even) in one v_cvt_pk_bf16_f32
+// two f32 -> packed bf16x2 (round-to-nearest-even): the vector conversion selects one
+// v_cvt_pk_bf16_f32 on gfx950.  (Not inline asm: the hazard recognizer does not check an asm's
+// VGPR operands against MFMAs in flight, so an asm def could land on an MFMA's source-C registers.)
+typedef __attribute__((ext_vector_type(2))) float f32x2_;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 VCAP_DEV uint32_t pack_bf2(float lo, float hi) {
-  uint32_t r;
-  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-  return r;
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){lo, hi}, bf16x2_t));
 }
 
 template <typename T> struct Num;
@@ -159,10 +161,11 @@ VCAP_DEV float wave_max(float v) { return rows_max(row16_max(v)); }
 
 // (value, index) argmax over the wave; ties resolve to the smallest index (torch.argmax order)
 VCAP_DEV void argmax_take(float& bv, int& bi, float ov, int oi) {
-  if (ov > bv || (ov == bv && oi < bi)) {
-    bv = ov;
-    bi = oi;
-  }
+  // bitwise, not short-circuit: `||` / `&&` here compiled to exec-mask branches (~14 scalar and
+  // vector instructions per take instead of 3 compares + 2 selects)
+  const bool t = (ov > bv) | ((ov == bv) & (oi < bi));
+  bv = t ? ov : bv;
+  bi = t ? oi : bi;
 }
 VCAP_DEV void wave_argmax(float& bv, int& bi) {
   argmax_take(bv, bi, dpp_f<DPP_XOR1>(bv), dpp_i<DPP_XOR1>(bi));

@@ -167,16 +167,17 @@ __global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __rest
 //  * Q fragments of all of a wave's query tiles are loaded before the K/V wait;
 //  * softmax: exp2 with (1/sqrt(64)) * log2(e) folded into one FMA, P packed to bf16 with
 //    v_cvt_pk_bf16_f32.
+// max of three as one v_max3_f32: this file is built with -fno-honor-nans (build.py), so maxnum
+// needs no operand canonicalisation.  (Not inline asm: the hazard recognizer does not see an asm
+// operand that overwrites the source-C registers of an MFMA still in flight.)
+VCAP_DEV float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+
 VCAP_DEV void glds16_attn(const void* g, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-VCAP_DEV uint32_t cvt_pk_bf16(float lo, float hi) {
-  uint32_t r;
-  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-  return r;
-}
+VCAP_DEV uint32_t cvt_pk_bf16(float lo, float hi) { return pack_bf2(lo, hi); }
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 
@@ -185,12 +186,181 @@ VCAP_DEV u32x2 tr_read(const char* p) {
   return __builtin_bit_cast(u32x2, v);
 }
 
+// One 16-query tile of one (frame, head): S^T = K.Q^T over the head's K image, exact softmax in
+// registers, O^T = V^T.P^T with V read by transpose reads.  Returns the unnormalised O^T fragments
+// and 1 / rowsum (lane (fr, fg) holds dims dt*16 + 4*fg + r of query fr).
+// KE: key tiles that can hold real keys (KT or KT - 1: with N <= 16 (KT - 1) the last tile is all
+// padding, kept only as the zero half of the last 32-key PV chunk - no S, max or exp for it).
+template <int KT, int KE>
+VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[2], int N, f32x4 (&o)[4],
+                              float& inv) {
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, fg = lane >> 4;
+  const float c2 = 0.125f * 1.4426950408889634f;  // 64^-0.5 * log2(e)
+  // S^T[key][q] = K . Q^T
+  f32x4 st[KT];
+  if constexpr (KE < KT) st[KT - 1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < KE; ++kt) {
+    f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int key = kt * 16 + fr;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const u32x4 kf = *reinterpret_cast<const u32x4*>(Ks + key * 128 + (((s * 4 + fg) ^ (key & 7)) << 4));
+      acc = mfma_frag(kf, qf[s], acc, (bf16_t*)nullptr);
+    }
+    st[kt] = acc;  // keys kt*16 + 4*fg + r, query fr
+  }
+  // padded keys: the dispatcher picks KT with 16 (KT - 2) < N <= 16 KT, so only the last two key
+  // tiles can hold them (a compile-time range: a runtime test per tile kept ~60 lane masks live
+  // and spilled them through v_writelane / v_readlane)
+#pragma unroll
+  for (int kt = KT - 2; kt < KE; ++kt) {
+    const int lim = N - kt * 16 - fg * 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st[kt][r] = r < lim ? st[kt][r] : -INFINITY;
+  }
+  // row max: two v_max3 per key tile; exp2 argument and row sum as packed f32 pairs
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < KE; ++kt) mx = max3f(max3f(mx, st[kt][0], st[kt][1]), st[kt][2], st[kt][3]);
+  mx = rows_max(mx);
+#ifdef VCAP_ATTN_PACKED_SOFTMAX
+  const f32x2 c2v = (f32x2){c2, c2}, nmx = (f32x2){-mx * c2, -mx * c2};
+  f32x2 sum2 = (f32x2){0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < KE; ++kt)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 a = pk_fma((f32x2){st[kt][2 * h], st[kt][2 * h + 1]}, c2v, nmx);
+      const f32x2 p = (f32x2){__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+      st[kt][2 * h] = p.x;
+      st[kt][2 * h + 1] = p.y;
+      sum2 += p;
+    }
+  const float sum = rows_sum(sum2.x + sum2.y);
+#else
+  const float mxc = mx * c2;
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < KE; ++kt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(st[kt][r], c2, -mxc));
+      st[kt][r] = p;
+      sum += p;
+    }
+  sum = rows_sum(sum);
+#endif
+
+  // O^T[d][q] = sum_key V[key][d] P^T[key][q]; k element j of lane group g <-> key
+  // 32c + 4g + j (j < 4) / 32c + 16 + 4g + (j - 4), matching the P^T fragment below
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int qr = fr >> 2, p4 = fr & 3;
+#pragma unroll
+  for (int c = 0; c < KT / 2; ++c) {
+    const u32x4 pf = (u32x4){cvt_pk_bf16(st[2 * c][0], st[2 * c][1]), cvt_pk_bf16(st[2 * c][2], st[2 * c][3]),
+                             cvt_pk_bf16(st[2 * c + 1][0], st[2 * c + 1][1]),
+                             cvt_pk_bf16(st[2 * c + 1][2], st[2 * c + 1][3])};
+    const int r0 = 32 * c + 4 * fg + qr, r1 = r0 + 16;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int ch = 2 * dt + (p4 >> 1);
+      const u32x2 lo = tr_read(Vs + r0 * 128 + ((ch ^ (r0 & 7)) << 4) + 8 * (p4 & 1));
+      const u32x2 hi = tr_read(Vs + r1 * 128 + ((ch ^ (r1 & 7)) << 4) + 8 * (p4 & 1));
+      o[dt] = mfma_frag((u32x4){lo.x, lo.y, hi.x, hi.y}, pf, o[dt], (bf16_t*)nullptr);
+    }
+  }
+  inv = 1.0f / sum;
+}
+
+// A query tile's output, packed for its stores: bf16 -> two dwordx4 per lane (lane pair exchange),
+// MXFP8 -> one dwordx4 per lane + the lane group 0 scale bytes.  Built right after the compute;
+// `attn_commit` stores it (the pipelined kernel defers that past its next loads).
+struct AttnOut {
+  u32x4 w0, w1;
+  int sb0, sb1;
+  long row;
+  bool keep;
+};
+
+template <bool MXO>
+VCAP_DEV AttnOut attn_pack(const f32x4 (&o)[4], float inv, long row, bool keep) {
+  const int lane = threadIdx.x & 63;
+  AttnOut r;
+  r.row = row;
+  r.keep = keep;
+  r.sb0 = r.sb1 = 0;
+  if constexpr (MXO) {
+    // block b = dims [32b, 32b+32) of the row: dt in {2b, 2b+1} of this lane and lanes fg = 0..3;
+    // after quantisation a 4x4 lane-group transpose hands every lane 16 contiguous bytes of the
+    // head's 64 (lane group g: dims [16g, 16g+16)), one dwordx4 store per lane
+    uint32_t x[4];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const f32x4 v0 = o[2 * b] * inv, v1 = o[2 * b + 1] * inv;
+      float amax = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fmaxf(fabsf(v0[e]), fabsf(v1[e])));
+      amax = rows_max(amax);
+      const int sb = mx_scale_byte(amax);
+      const float is = mx_inv_scale(sb);
+      x[2 * b] = pack_fp8x4(v0.x * is, v0.y * is, v0.z * is, v0.w * is);
+      x[2 * b + 1] = pack_fp8x4(v1.x * is, v1.y * is, v1.z * is, v1.w * is);
+      if (b == 0) r.sb0 = sb; else r.sb1 = sb;
+    }
+    transpose4_groups(x);
+    r.w0 = (u32x4){x[0], x[1], x[2], x[3]};
+    r.w1 = r.w0;
+  } else {
+    // O[q][d = dt*16 + 4*fg + r]; lanes fg, fg ^ 1 (lane ^ 16) trade halves of the dt pair
+    // (2k, 2k+1) so each stores 8 contiguous dims with one dwordx4 (the even lane dims
+    // [32k + 4fg, +8), the odd lane [32k + 12 + 4fg, +8)); the exchange runs in every lane
+    const bool odd = (lane & 16) != 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const f32x4 va = o[2 * k] * inv, vb = o[2 * k + 1] * inv;
+      const uint32_t a0 = cvt_pk_bf16(va.x, va.y), a1 = cvt_pk_bf16(va.z, va.w);
+      const uint32_t b0 = cvt_pk_bf16(vb.x, vb.y), b1 = cvt_pk_bf16(vb.z, vb.w);
+      const uint32_t r0 = (uint32_t)xor16_i((int)(odd ? a0 : b0));
+      const uint32_t r1 = (uint32_t)xor16_i((int)(odd ? a1 : b1));
+      const u32x4 w = odd ? (u32x4){r0, r1, b0, b1} : (u32x4){a0, a1, r0, r1};
+      if (k == 0) r.w0 = w; else r.w1 = w;
+    }
+  }
+  return r;
+}
+
+template <bool MXO>
+VCAP_DEV void attn_commit(const AttnOut& r, void* out, int D, int h, uint8_t* oscale, int groups) {
+  if (!r.keep) return;
+  const int lane = threadIdx.x & 63, fg = lane >> 4;
+  if constexpr (MXO) {
+    if (fg == 0) {
+      oscale[mx_scale_index((int)r.row, h * 64, groups)] = (uint8_t)r.sb0;
+      oscale[mx_scale_index((int)r.row, h * 64 + 32, groups)] = (uint8_t)r.sb1;
+    }
+    *reinterpret_cast<u32x4*>((uint8_t*)out + r.row * D + h * 64 + 16 * fg) = r.w0;
+  } else {
+    const bool odd = (lane & 16) != 0;
+    bf16_t* orow = (bf16_t*)out + r.row * D + h * 64;
+#ifdef VCAP_NT_MORE
+    __builtin_nontemporal_store(r.w0, reinterpret_cast<u32x4*>(orow + (odd ? 12 + 4 * fg : 4 * fg)));
+    __builtin_nontemporal_store(r.w1, reinterpret_cast<u32x4*>(orow + 32 + (odd ? 12 + 4 * fg : 4 * fg)));
+#else
+    *reinterpret_cast<u32x4*>(orow + (odd ? 12 + 4 * fg : 4 * fg)) = r.w0;
+    *reinterpret_cast<u32x4*>(orow + 32 + (odd ? 12 + 4 * fg : 4 * fg)) = r.w1;
+#endif
+  }
+}
+
 // One workgroup per (frame, head) pair; two of them share a CU (56 KiB of LDS, <= 128 VGPRs
-// for 4 waves per SIMD), so one pair's DMA overlaps the other's MFMA / softmax.  (A persistent
-// double-buffered variant measured slower: its doubled Q registers cost half the occupancy.)
+// for 4 waves per SIMD), so one pair's DMA overlaps the other's MFMA / softmax.  Used for the
+// CLS-only last block, the L/14 shapes and (VCAP_ATTN_PIPE=0) everywhere.
 // MXO: write the output as MXFP8 (e4m3 + E8M0 per 32 of the head's 64 dims) for an MXFP8 attn-proj
 // GEMM; oscale in the vcap_common.h layout over `groups` 256-row groups.
-template <int KT, int WAVES, bool MXO>
+template <int KT, int KE, int WAVES, bool MXO>
 __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(const bf16_t* __restrict__ qkv,
                                                                              void* __restrict__ out, int N, int H,
                                                                              uint8_t* __restrict__ oscale,
@@ -212,6 +382,7 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
   const int fr = lane & 15, fg = lane >> 4;
 
   // ---- K, V -> LDS by DMA (rows past N re-read row N-1: finite, masked out of the softmax)
+#ifndef VCAP_DIAG_ATTN_NOLOAD
   for (int blk = wave; blk < NP / 8; blk += WAVES) {
     const int r = blk * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (r & 7);
@@ -219,6 +390,7 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
     glds16_attn(src + D, Ks + blk * 1024);
     glds16_attn(src + 2 * D, Vs + blk * 1024);
   }
+#endif
   // ---- this wave's Q fragments
   const int qtiles = cls_only ? 1 : (N + 15) / 16;
   u32x4 qf[QT_MAX][2];
@@ -231,125 +403,148 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  const float c2 = 0.125f * 1.4426950408889634f;  // 64^-0.5 * log2(e)
 #pragma unroll
   for (int i = 0; i < QT_MAX; ++i) {
     const int qt = wave + i * WAVES;
     if (qt >= qtiles) break;
-    // S^T[key][q] = K . Q^T
-    f32x4 st[KT];
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-      f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-      const int key = kt * 16 + fr;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const u32x4 kf = *reinterpret_cast<const u32x4*>(Ks + key * 128 + (((s * 4 + fg) ^ (key & 7)) << 4));
-        acc = mfma_frag(kf, qf[i][s], acc, (bf16_t*)nullptr);
-      }
-      st[kt] = acc;  // keys kt*16 + 4*fg + r, query fr
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-      if (kt * 16 + 16 > N) {  // wave-uniform: only the tail tiles hold padded keys
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (kt * 16 + fg * 4 + r >= N) st[kt][r] = -INFINITY;
-      }
-      mx = fmaxf(mx, fmaxf(fmaxf(st[kt][0], st[kt][1]), fmaxf(st[kt][2], st[kt][3])));
-    }
-    mx = rows_max(mx);
-    const float mxc = mx * c2;
-    float sum = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(st[kt][r], c2, -mxc));
-        st[kt][r] = p;
-        sum += p;
-      }
-    sum = rows_sum(sum);
-
-    // O^T[d][q] = sum_key V[key][d] P^T[key][q]; k element j of lane group g <-> key
-    // 32c + 4g + j (j < 4) / 32c + 16 + 4g + (j - 4), matching the P^T fragment below
     f32x4 o[4];
-#pragma unroll
+    float inv;
+#ifdef VCAP_DIAG_ATTN_NOCOMP
     for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int qr = fr >> 2, p4 = fr & 3;
-#pragma unroll
-    for (int c = 0; c < KT / 2; ++c) {
-      const u32x4 pf = (u32x4){cvt_pk_bf16(st[2 * c][0], st[2 * c][1]), cvt_pk_bf16(st[2 * c][2], st[2 * c][3]),
-                               cvt_pk_bf16(st[2 * c + 1][0], st[2 * c + 1][1]),
-                               cvt_pk_bf16(st[2 * c + 1][2], st[2 * c + 1][3])};
-      const int r0 = 32 * c + 4 * fg + qr, r1 = r0 + 16;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int ch = 2 * dt + (p4 >> 1);
-        const u32x2 lo = tr_read(Vs + r0 * 128 + ((ch ^ (r0 & 7)) << 4) + 8 * (p4 & 1));
-        const u32x2 hi = tr_read(Vs + r1 * 128 + ((ch ^ (r1 & 7)) << 4) + 8 * (p4 & 1));
-        o[dt] = mfma_frag((u32x4){lo.x, lo.y, hi.x, hi.y}, pf, o[dt], (bf16_t*)nullptr);
-      }
-    }
+    inv = 1.f;
+#else
+    attn_bf16_qtile<KT, KE>(Ks, Vs, qf[i], N, o, inv);
+#endif
     const int q = qt * 16 + fr;
-    const float inv = 1.0f / sum;
     const bool keep = q < N && (!cls_only || q == 0);
     const long row = cls_only ? (long)bt : (long)bt * N + q;
-    if constexpr (MXO) {
-      // block b = dims [32b, 32b+32) of row q: dt in {2b, 2b+1} of this lane and lanes fg = 0..3;
-      // after quantisation a 4x4 lane-group transpose hands every lane 16 contiguous bytes of the
-      // head's 64 (lane group g: dims [16g, 16g+16)), one dwordx4 store per lane
-      uint32_t x[4];
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const f32x4 v0 = o[2 * b] * inv, v1 = o[2 * b + 1] * inv;
-        float amax = 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fmaxf(fabsf(v0[e]), fabsf(v1[e])));
-        amax = rows_max(amax);
-        const int sb = mx_scale_byte(amax);
-        const float is = mx_inv_scale(sb);
-        x[2 * b] = pack_fp8x4(v0.x * is, v0.y * is, v0.z * is, v0.w * is);
-        x[2 * b + 1] = pack_fp8x4(v1.x * is, v1.y * is, v1.z * is, v1.w * is);
-        if (keep && fg == 0) oscale[mx_scale_index((int)row, h * 64 + 32 * b, groups)] = (uint8_t)sb;
-      }
-      transpose4_groups(x);
-      if (keep)
-        *reinterpret_cast<u32x4*>((uint8_t*)out + row * D + h * 64 + 16 * fg) = (u32x4){x[0], x[1], x[2], x[3]};
-    } else {
-      // O[q][d = dt*16 + 4*fg + r]; lanes fg, fg ^ 1 (lane ^ 16) trade halves of the dt pair
-      // (2k, 2k+1) so each stores 8 contiguous dims with one dwordx4 (the even lane dims
-      // [32k + 4fg, +8), the odd lane [32k + 12 + 4fg, +8)); the exchange runs in every lane
-      const bool odd = (threadIdx.x & 16) != 0;
-      bf16_t* orow = (bf16_t*)out + row * D + h * 64;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const f32x4 va = o[2 * k] * inv, vb = o[2 * k + 1] * inv;
-        const uint32_t a0 = cvt_pk_bf16(va.x, va.y), a1 = cvt_pk_bf16(va.z, va.w);
-        const uint32_t b0 = cvt_pk_bf16(vb.x, vb.y), b1 = cvt_pk_bf16(vb.z, vb.w);
-        const uint32_t r0 = (uint32_t)xor16_i((int)(odd ? a0 : b0));
-        const uint32_t r1 = (uint32_t)xor16_i((int)(odd ? a1 : b1));
-        const u32x4 w = odd ? (u32x4){r0, r1, b0, b1} : (u32x4){a0, a1, r0, r1};
-        if (keep) *reinterpret_cast<u32x4*>(orow + 32 * k + (odd ? 12 + 4 * fg : 4 * fg)) = w;
-      }
-    }
+    attn_commit<MXO>(attn_pack<MXO>(o, inv, row, keep), out, D, h, oscale, groups);
   }
 }
 
-template <int KT, int WAVES, bool MXO>
+// Pipelined variant for the full-sequence blocks: one workgroup per CU walks (frame, head) items
+// blockIdx.x, + gridDim.x, ...  K / V images are double-buffered and Q is staged in LDS too, so
+// while the waves compute item i the DMA of item i + 1 is in flight, and item i - 1's output
+// stores are issued right after that DMA (the vector memory counter is in order, so stores issued
+// before the next wait would otherwise be waited on with the loads).  One query tile per wave.
+template <int KT, int KE, int WAVES, bool MXO>
+__global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_pipe_kernel(const bf16_t* __restrict__ qkv,
+                                                                             void* __restrict__ out, int N, int H,
+                                                                             int items, uint8_t* __restrict__ oscale,
+                                                                             int groups) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NP = KT * 16;
+  constexpr int QP = (KT - 1) * 16;  // staged query rows (N > NP - 16 -> (N + 15) / 16 == KT - 1 tiles)
+  static_assert(KT % 2 == 0 && KT - 1 <= WAVES, "one query tile per wave");
+  char* Q = smem + 4 * NP * 128;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int qtiles = (N + 15) / 16;
+
+  auto issue = [&](int item, int buf) {
+#ifdef VCAP_DIAG_ATTN_NOLOAD
+    return;
+#endif
+    const int bt = item / H, h = item - bt * H;
+    const bf16_t* base = qkv + (long)bt * N * ld + h * 64;
+    char* Ks = smem + buf * 2 * NP * 128;
+    char* Vs = Ks + NP * 128;
+    for (int blk = wave; blk < NP / 8; blk += WAVES) {
+      const int r = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      const bf16_t* src = base + (long)min(r, N - 1) * ld + c * 8;
+      glds16_attn(src + D, Ks + blk * 1024);
+      glds16_attn(src + 2 * D, Vs + blk * 1024);
+    }
+    for (int blk = wave; blk < QP / 8; blk += WAVES) {
+      const int r = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      glds16_attn(base + (long)min(r, N - 1) * ld + c * 8, Q + blk * 1024);
+    }
+  };
+
+  int item = blockIdx.x, buf = 0;
+  if (item < items) issue(item, 0);
+  AttnOut pend;
+  pend.keep = false;
+  int pend_h = 0;
+  for (; item < items; item += gridDim.x, buf ^= 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // item's K / V / Q landed for every wave
+    const int qt = wave;
+    const int qrow = qt * 16 + fr;
+    u32x4 qf[2] = {(u32x4){0u, 0u, 0u, 0u}, (u32x4){0u, 0u, 0u, 0u}};
+    if (qt < qtiles) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        qf[s] = *reinterpret_cast<const u32x4*>(Q + qrow * 128 + (((s * 4 + fg) ^ (qrow & 7)) << 4));
+    }
+    __syncthreads();  // Q image free for the next item
+    const int next = item + gridDim.x;
+    if (next < items) issue(next, buf ^ 1);
+    attn_commit<MXO>(pend, out, D, pend_h, oscale, groups);
+    pend.keep = false;
+    if (qt < qtiles) {
+      const char* Ks = smem + buf * 2 * NP * 128;
+      f32x4 o[4];
+      float inv;
+#ifdef VCAP_DIAG_ATTN_NOCOMP
+      for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      inv = 1.f;
+#else
+      attn_bf16_qtile<KT, KE>(Ks, Ks + NP * 128, qf, N, o, inv);
+#endif
+      const int bt = item / H;
+      pend = attn_pack<MXO>(o, inv, (long)bt * N + qrow, qrow < N);
+      pend_h = item - bt * H;
+    }
+  }
+  attn_commit<MXO>(pend, out, D, pend_h, oscale, groups);
+}
+
+template <int KT, int KE, int WAVES, bool MXO>
+static hipError_t launch_attn_pipe(const void* qkv, void* out, int BT, int N, int H, uint8_t* oscale,
+                                   hipStream_t s) {
+  const size_t lds = (size_t)4 * KT * 16 * 128 + (size_t)(KT - 1) * 16 * 128;
+  static bool configured = false;
+  if (!configured) {
+    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_pipe_kernel<KT, KE, WAVES, MXO>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    configured = true;
+  }
+  const int items = BT * H;
+  const int groups = (BT * N + 255) / 256;
+  const int grid = std::min(items, vcap_device_cus());
+  hipLaunchKernelGGL((vcap_vit_attention_pipe_kernel<KT, KE, WAVES, MXO>), dim3(grid), dim3(WAVES * 64), lds, s,
+                     (const bf16_t*)qkv, out, N, H, items, oscale, groups);
+  return hipGetLastError();
+}
+
+static bool attn_pipe_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VCAP_ATTN_PIPE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+template <int KT, int KE, int WAVES, bool MXO>
 static hipError_t launch_attn_bf16(const void* qkv, void* out, int BT, int N, int H, uint8_t* oscale, int cls_only,
                                    hipStream_t s) {
   const size_t lds = (size_t)KT * 16 * 128 * 2;
   static bool configured = false;
   if (!configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_bf16_kernel<KT, WAVES, MXO>,
+    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_bf16_kernel<KT, KE, WAVES, MXO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     configured = true;
   }
   const int groups = ((cls_only ? BT : BT * N) + 255) / 256;  // scale rows = output rows
-  hipLaunchKernelGGL((vcap_vit_attention_bf16_kernel<KT, WAVES, MXO>), dim3(BT * H), dim3(WAVES * 64), lds, s,
+  hipLaunchKernelGGL((vcap_vit_attention_bf16_kernel<KT, KE, WAVES, MXO>), dim3(BT * H), dim3(WAVES * 64), lds, s,
                      (const bf16_t*)qkv, out, N, H, oscale, groups, cls_only);
   return hipGetLastError();
 }
@@ -371,19 +566,32 @@ static hipError_t launch_attn(const void* qkv, void* out, int BT, int N, int H, 
   return hipGetLastError();
 }
 
+// bf16 kernel choice: the pipelined walk for the full-sequence ViT-B/16 blocks (13 query tiles),
+// the per-(frame, head) kernel otherwise; KE = key tiles that can hold real keys
+template <bool MXO>
+static hipError_t attn_bf16_dispatch(const void* qkv, void* out, uint8_t* oscale, int BT, int N, int H,
+                                     int cls_only, hipStream_t s) {
+  switch (((N + 31) / 32) * 2) {  // keys padded to a multiple of 32
+    case 2: return launch_attn_bf16<2, 2, 4, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
+    case 14:
+      if (N <= 13 * 16) {
+        if (!cls_only && N > 12 * 16 && attn_pipe_enabled())
+          return launch_attn_pipe<14, 13, 16, MXO>(qkv, out, BT, N, H, oscale, s);
+        return launch_attn_bf16<14, 13, 8, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
+      }
+      return launch_attn_bf16<14, 14, 8, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
+    case 18:
+      if (N <= 17 * 16) return launch_attn_bf16<18, 17, 8, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
+      return launch_attn_bf16<18, 18, 8, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s,
                                        int cls_only) {
   if (N <= 0 || N > 288) return hipErrorInvalidValue;
-  const int kt = ((N + 31) / 32) * 2;  // keys padded to a multiple of 32
-  if (dt == VCAP_DT_BF16) {
-    switch (kt) {
-      case 2: return launch_attn_bf16<2, 4, false>(qkv, out, BT, N, H, nullptr, cls_only, s);
-      case 14: return launch_attn_bf16<14, 8, false>(qkv, out, BT, N, H, nullptr, cls_only, s);
-      case 18: return launch_attn_bf16<18, 8, false>(qkv, out, BT, N, H, nullptr, cls_only, s);
-      default: return hipErrorInvalidValue;
-    }
-  }
-  switch (kt) {
+  if (dt == VCAP_DT_BF16) return attn_bf16_dispatch<false>(qkv, out, nullptr, BT, N, H, cls_only, s);
+  switch (((N + 31) / 32) * 2) {
     case 2: return launch_attn<float, 2>(qkv, out, BT, N, H, cls_only, s);
     case 14: return launch_attn<float, 14>(qkv, out, BT, N, H, cls_only, s);
     case 18: return launch_attn<float, 18>(qkv, out, BT, N, H, cls_only, s);
@@ -395,10 +603,5 @@ hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int B
 hipError_t vcap_vit_attention_mx_dispatch(const void* qkv, void* out, uint8_t* oscale, int BT, int N, int H,
                                           hipStream_t s, int cls_only) {
   if (N <= 0 || N > 288 || !oscale) return hipErrorInvalidValue;
-  switch (((N + 31) / 32) * 2) {
-    case 2: return launch_attn_bf16<2, 4, true>(qkv, out, BT, N, H, oscale, cls_only, s);
-    case 14: return launch_attn_bf16<14, 8, true>(qkv, out, BT, N, H, oscale, cls_only, s);
-    case 18: return launch_attn_bf16<18, 8, true>(qkv, out, BT, N, H, oscale, cls_only, s);
-    default: return hipErrorInvalidValue;
-  }
+  return attn_bf16_dispatch<true>(qkv, out, oscale, BT, N, H, cls_only, s);
 }

@@ -26,6 +26,11 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-at
          "-Wno-unused-result", f"-I{CSRC}", f"-I{INCLUDE}"] + os.environ.get("VCAP_EXTRA_FLAGS", "").split()
 
 
+# per-file flags: the attention softmax never sees a NaN (masked keys are -inf), and without
+# -fno-honor-nans every fmaxf of an MFMA result is preceded by a canonicalising v_max
+FILE_FLAGS = {"vit_attention.hip": ["-fno-honor-nans"]}
+
+
 def sources():
     return sorted(CSRC.glob("*.hip"))
 
@@ -36,11 +41,12 @@ def _digest() -> str:
         h.update(p.name.encode())
         h.update(p.read_bytes())
     h.update(" ".join(FLAGS).encode())
+    h.update(repr(sorted(FILE_FLAGS.items())).encode())
     return h.hexdigest()
 
 
 def _compile(src: Path, obj: Path):
-    cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")

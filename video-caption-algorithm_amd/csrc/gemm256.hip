@@ -76,26 +76,14 @@ VCAP_DEV u32x4 frag(const char* half, int row, int chunk) {
   return *reinterpret_cast<const u32x4*>(half + row * ROWB + ((chunk ^ (row & 7)) << 4));
 }
 
-// Output stores are streaming (nontemporal): a round's 128 KiB-per-CU write-back then does not
-// evict the A row panels / W tiles the next round re-reads from L2 (fc1 135.7 -> 127.5 us,
-// QKV 100 -> 97 us alone; profiles/r02_gemm_nt_store_ab.txt).
+// bf16 / MXFP8 output stores are streaming (nontemporal): a round's 128 KiB-per-CU write-back then
+// does not evict the A row panels / W tiles the next round re-reads from L2 (fc1 135.7 -> 127.5 us,
+// QKV 100 -> 97 us alone).  The in-place f32 residual stores stay plain (the LayerNorm reads them
+// next: 1097 -> 1102 captions/s).  profiles/r02_gemm_nt_store_ab.txt.
 template <typename V>
 VCAP_DEV void out_store(V* p, const V& v) {
-#ifdef VCAP_GEMM_PLAIN_STORE
-  *p = v;
-#else
-  __builtin_nontemporal_store(v, p);
-#endif
-}
-
-// read-once operand (the in-place residual)
-template <typename V>
-VCAP_DEV V once_load(const V* p) {
-#ifdef VCAP_NT_MORE
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
+  if constexpr (__is_same(V, f32x4)) *p = v;
+  else __builtin_nontemporal_store(v, p);
 }
 
 VCAP_DEV void lds_fence() { asm volatile("" ::: "memory"); }
@@ -428,13 +416,13 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
           } else if constexpr (EPI == 2) {
-            v += once_load(reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n));
+            v += *reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n);
           } else if constexpr (EPI == 3) {
             if (epi.act == 1)
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
             orow = epi.G ? (long)(m / epi.G) * epi.Gs + epi.goff + (m % epi.G) : (long)m;
-            if (epi.res_mode == 1) v += once_load(reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n));
+            if (epi.res_mode == 1) v += *reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n);
             else if (epi.res_mode == 2)
               v += *reinterpret_cast<const f32x4*>(epi.res + (long)((m % epi.G) + epi.roff) * epi.ldr + n);
           }

@@ -50,11 +50,7 @@ __global__ __launch_bounds__(256) void vcap_layernorm_kernel(const float* __rest
           o = o * g + b;
         }
         if constexpr (sizeof(TOut) == 2) {
-#ifdef VCAP_NT_MORE
-          __builtin_nontemporal_store((u32x2){pack_bf2(o.x, o.y), pack_bf2(o.z, o.w)}, reinterpret_cast<u32x2*>(yr + c));
-#else
           *reinterpret_cast<u32x2*>(yr + c) = (u32x2){pack_bf2(o.x, o.y), pack_bf2(o.z, o.w)};
-#endif
         } else {
           *reinterpret_cast<f32x4*>(yr + c) = o;
         }

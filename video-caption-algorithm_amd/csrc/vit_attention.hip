@@ -345,13 +345,8 @@ VCAP_DEV void attn_commit(const AttnOut& r, void* out, int D, int h, uint8_t* os
   } else {
     const bool odd = (lane & 16) != 0;
     bf16_t* orow = (bf16_t*)out + r.row * D + h * 64;
-#ifdef VCAP_NT_MORE
-    __builtin_nontemporal_store(r.w0, reinterpret_cast<u32x4*>(orow + (odd ? 12 + 4 * fg : 4 * fg)));
-    __builtin_nontemporal_store(r.w1, reinterpret_cast<u32x4*>(orow + 32 + (odd ? 12 + 4 * fg : 4 * fg)));
-#else
     *reinterpret_cast<u32x4*>(orow + (odd ? 12 + 4 * fg : 4 * fg)) = r.w0;
     *reinterpret_cast<u32x4*>(orow + 32 + (odd ? 12 + 4 * fg : 4 * fg)) = r.w1;
-#endif
   }
 }
 

@@ -66,6 +66,8 @@ def parse():
                     help="decodes in flight at once (own stream + workspace + graph each)")
     ap.add_argument("--dec-group", type=int, default=2,
                     help="consecutive batches decoded together as one decode of group*batch rows")
+    ap.add_argument("--enc-group", type=int, default=2,
+                    help="consecutive batches encoded together as one encode (divides --dec-group)")
     ap.add_argument("--confine-decode", action="store_true",
                     help="mask the decode streams to the reserved CUs (default: unmasked, high priority)")
     ap.add_argument("--gemm-policy", type=int, default=0, help="vcap_set_gemm_policy value for A/B runs (0 = auto)")
@@ -124,33 +126,45 @@ def cpu_baseline(sd, va, ga, frames_np, budget_s: float, max_new: int, beams: in
     return out
 
 
+PMC_FILES = ("r02_pmc.json", "r01_pmc.json")   # newest first
+
+
+def _pmc_file(M: int):
+    """The committed rocprofv3 PMC summary (tools/pmc.sh + tools/pmc_report.py) collected on ViT
+    GEMM launches of M rows, or None (PMC counters cannot be read inside bench.py)."""
+    for name in PMC_FILES:
+        try:
+            d = json.loads((ROOT / "profiles" / name).read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("vit_rows", 25216) == M:
+            return name, d
+    return None, None
+
+
 def fc1_traffic(M: int, N: int, K: int):
-    """HBM bytes per fc1 launch from the committed rocprofv3 PMC passes (profiles/), when they were
-    collected on this exact shape; None otherwise (PMC counters cannot be read inside bench.py)."""
-    p = ROOT / "profiles" / "r01_fc1_pmc_traffic.json"
-    try:
-        d = json.loads(p.read_text())
-    except (OSError, ValueError):
+    """HBM bytes per fc1 launch (FETCH_SIZE x2 + WRITE_SIZE) from the committed PMC passes, when
+    they were collected on this exact shape; None otherwise."""
+    name, d = _pmc_file(M)
+    if d is None or (N, K) != (3072, 768):
         return None
-    if d.get("shape") != {"M": M, "N": N, "K": K}:
+    k = next((v for n, v in d["vit_kernels"].items() if "gemm256_kernel<unsigned short, unsigned short, 1>" in n), None)
+    if not k or k.get("fetch_bytes") is None or k.get("write_bytes") is None:
         return None
-    b = d["per_launch_bytes"]
-    return float(b["fetch"] + b["write"])
+    return float(k["fetch_bytes"] + k["write_bytes"])
 
 
-def pmc_summary(vit: str, gpt2: str, B: int, T: int, precision: str):
+def pmc_summary(vit: str, gpt2: str, M: int, precision: str):
     """MFMA utilisation of the ViT GEMMs and the decode's HBM bytes per token step from the
-    committed rocprofv3 PMC passes (profiles/r01_pmc.json: tools/pmc.sh + tools/pmc_report.py on
-    this configs[1] workload); None for other workloads (counters cannot be read in bench.py)."""
-    if (vit, gpt2, B, T, precision) != ("vit_base_patch16_224", "gpt2", 8, 16, "bf16"):
+    committed PMC passes on this configs[1] workload; None for other workloads."""
+    if (vit, gpt2, precision) != ("vit_base_patch16_224", "gpt2", "bf16"):
         return None
-    try:
-        d = json.loads((ROOT / "profiles" / "r01_pmc.json").read_text())
-    except (OSError, ValueError):
+    name, d = _pmc_file(M)
+    if d is None:
         return None
     util = {k.split("<", 1)[1].rstrip(">"): round(v["mfma_util"], 3) for k, v in d["vit_kernels"].items()
             if "gemm256" in k and v.get("mfma_util")}
-    return {"source": "profiles/r01_pmc.json (rocprofv3 --pmc, separate passes)",
+    return {"source": f"profiles/{name} (rocprofv3 --pmc, separate passes, ViT launches of {M} rows)",
             "vit_gemm_mfma_util": util,
             "decode_hbm_bytes_per_token_step": d["decode"]["hbm_bytes_per_token_step"]}
 
@@ -257,7 +271,8 @@ def main():
                            reserve_cus=0 if args.serial else args.reserve_cus,
                            dec_lanes=1 if args.serial else args.dec_lanes,
                            confine_decode=args.confine_decode and not args.serial,
-                           dec_group=1 if args.serial else args.dec_group)
+                           dec_group=1 if args.serial else args.dec_group,
+                           enc_group=1 if args.serial else args.enc_group)
 
     def step(t0=None, t1=None, t2=None):
         pipe.submit(video, t0, t1, t2)
@@ -359,12 +374,13 @@ def main():
     N.check(lib.vcap_probe_read(b"vit.attention", N.C.byref(at_total), N.C.byref(at_n)), "probe read")
 
     if rank == 0:
-        M = B * T * va.tokens
+        E = 1 if args.serial else args.enc_group   # batches per encode launch
+        M = E * B * T * va.tokens                    # ViT rows per GEMM launch
         fc1_flops = 2.0 * M * va.mlp * va.dim
         fc1_avg_s = fc1_total.value / max(fc1_n.value, 1) / 1e3
         peak = {"bf16": PEAK_BF16_TFLOPS, "fp8": PEAK_FP8_TFLOPS}.get(args.precision, PEAK_F32_TFLOPS)
         achieved = fc1_flops / fc1_avg_s / 1e12
-        attn_flops = 4.0 * B * T * va.heads * va.tokens * va.tokens * 64
+        attn_flops = 4.0 * E * B * T * va.heads * va.tokens * va.tokens * 64
         attn_avg_s = at_total.value / max(at_n.value, 1) / 1e3
         ab = 2 if args.precision in ("bf16", "fp8") else 4
         attn_bytes = float(M * 3 * va.dim * ab + M * va.dim * (1 if args.precision == "fp8" else ab))
@@ -390,11 +406,13 @@ def main():
                        "decode_block_cap": cfg.max_blocks,
                        "schedule": "serial" if args.serial else
                        f"CU-masked encode stream (off {args.reserve_cus} CUs) overlapped with {args.dec_lanes} decode "
-                       f"lane(s) in flight; each decode = {args.dec_group} consecutive batch(es) as one "
+                       f"lane(s) in flight; each encode = {args.enc_group} consecutive batch(es) as one "
+                       f"{args.enc_group * B}-video encode; each decode = {args.dec_group} consecutive batch(es) as one "
                        + (f"{args.dec_group * B}-row greedy decode graph" if args.beams == 1 else
                           f"{args.dec_group * B} x {args.beams}-beam search graph"),
                        "dec_lanes": 1 if args.serial else args.dec_lanes,
-                       "dec_group": 1 if args.serial else args.dec_group},
+                       "dec_group": 1 if args.serial else args.dec_group,
+                       "enc_group": 1 if args.serial else args.enc_group},
             "value_definition": "pipelined throughput: videos captioned / wall time of the timed steps "
                                 "(encodes overlapped with the decodes of earlier batches)",
             "captions_per_s_b_over_p50": world * B / (p50 / 1e3),
@@ -424,7 +442,7 @@ def main():
             "path_roofline": {"t_roof_ms": t_roof * 1e3, "t_measured_ms": elapsed / args.steps * 1e3,
                               "frac": t_roof / (elapsed / args.steps),
                               "vit_tflop": vit_exec / 1e12, "decode_weight_gb": dec_bytes / 1e9},
-            "pmc": pmc_summary(args.vit, args.gpt2, B, T, args.precision),
+            "pmc": pmc_summary(args.vit, args.gpt2, M, args.precision),
             "parity": parity,
             "decode_roofline": dec_alone,
             "vit_flops_per_step": B * T * va.flops_per_frame(),

@@ -143,12 +143,13 @@ def test_lm_head_processor_epilogue_every_step(device, prec):
         fin |= ids64[:, s] == eos
 
 
-@pytest.mark.parametrize("lanes,group", [(2, 1), (1, 2), (2, 2), (1, 4)])
-def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group):
+@pytest.mark.parametrize("lanes,group,egroup", [(2, 1, 1), (1, 2, 1), (2, 2, 1), (1, 4, 1), (2, 2, 2), (1, 4, 2)])
+def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group, egroup):
     """The bench schedule (vcap/pipeline.py: CU-masked encode stream, decode lanes with capped
     grids, own workspaces / graphs, optionally `group` batches decoded as one decode of group*8
-    rows) gives bit-identical bf16 encodes and ids to a serial bf16 encode + generate_ids on the
-    default stream (deterministic split-K, mask-independent plans, row-independent decode)."""
+    rows and `egroup` batches encoded as one encode of egroup*8 videos) gives bit-identical bf16
+    encodes and ids to a serial bf16 encode + generate_ids of one batch on the default stream
+    (deterministic, M-independent split-K; mask-independent plans; row-independent kernels)."""
     from vcap.pipeline import CaptionPipeline
     meta, g, va, ga, sd, frames, enc, pre, dec = _models("bf16", device)
     video = torch.from_numpy(frames).to(device)
@@ -156,7 +157,7 @@ def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group):
     ids_serial = dec.generate_ids(pre_serial, [ga.bos_token_id], _hf_cfg(ga)).clone()
     cfg = _hf_cfg(ga, max_blocks=128)
     pipe = CaptionPipeline(enc, pre, dec, cfg, video.shape[0], [ga.bos_token_id], device, reserve_cus=32,
-                           dec_lanes=lanes, dec_group=group)
+                           dec_lanes=lanes, dec_group=group, enc_group=egroup)
     try:
         slots = [pipe.submit(video) for _ in range(5)]
         pipe.synchronize()

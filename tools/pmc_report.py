@@ -2,7 +2,7 @@
 per-kernel FETCH/WRITE bytes (FETCH_SIZE doubled: gfx950 reports half of 16-B-per-lane streaming
 reads, MI355X_MICROARCH.md), MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x
 GRBM_GUI_ACTIVE / 8 XCDs), LDS bank conflicts; plus the decode's HBM bytes per token step.
-usage: python tools/pmc_report.py <pmc outdir> <token steps in the run> <out.json>"""
+usage: python tools/pmc_report.py <pmc outdir> <token steps in the run> <out.json> [ViT rows per launch]"""
 import csv
 import glob
 import json
@@ -10,6 +10,7 @@ import sys
 from collections import defaultdict
 
 out_dir, token_steps, dst = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+vit_rows = int(sys.argv[4]) if len(sys.argv) > 4 else 25216
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(f"{out_dir}/*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -36,6 +37,7 @@ for name, c in acc.items():
         dec_bytes += (sum(c["FETCH_SIZE"]) * 2 + sum(c.get("WRITE_SIZE", [0]))) * 1000
 vit = {k: v for k, v in kernels.items() if "gemm256" in k or "vit_attention" in k or "layernorm" in k}
 res = {"source": "rocprofv3 --pmc passes (tools/pmc.sh) of python bench.py --serial --steps 2 --warmup 1",
+       "vit_rows": vit_rows,
        "vit_kernels": vit,
        "decode": {"token_steps": token_steps, "hbm_bytes_per_token_step": dec_bytes / token_steps,
                   "algorithmic_weight_bytes_per_token_step": 247.1e6,

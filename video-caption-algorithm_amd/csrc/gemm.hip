@@ -201,24 +201,24 @@ static hipError_t launch_gemm_epi(const void* A, long lda, const void* W, long l
   // Few tiles (the CLS-only last block: M = B*T rows) leave most CUs idle through a long K
   // loop: split K over several workgroups per tile when C is f32 and already holds the
   // residual (attn-proj / fc2 in place) and the caller gave a partials workspace (bf16 operands
-  // only: the fp32 parity mode keeps one summation chain).  The plan depends on the shape and
-  // the DEVICE's CU count only, never on the stream's CU mask, so a CU-masked pipelined encode
-  // sums exactly like a serial one.
+  // only: the fp32 parity mode keeps one summation chain).  The split count depends on K alone
+  // (the largest divisor c <= 8 of the K-tile count leaving >= 3 K-tiles per workgroup), never on
+  // M or the stream's CU mask, so a row sums the same way whichever batch it is encoded in and a
+  // CU-masked pipelined encode sums exactly like a serial one.
   int splits = 1;
   if constexpr (sizeof(TIn) == 2 && sizeof(TOut) == 4) {
     const bool in_place = epi.bias != nullptr && epi.res == (const float*)C && epi.ldr == ldc &&
                           (EPI == 2 || (EPI == 3 && epi.res_mode == 1 && epi.act == 0)) && epi.splitk_ws &&
                           (N & 3) == 0 && (ldc & 3) == 0 && ((uintptr_t)C & 15) == 0;
     const int nkt = K / (ROWB / (int)sizeof(TIn));
-    const int ncu = vcap_device_cus();
-    // keep >= 3 K-tiles per workgroup and the grid within a quarter of the CUs
-    if (in_place && tiles * 8 <= ncu)
-      for (int c = 16; c >= 2; --c)
-        if (nkt % c == 0 && nkt / c >= 3 && tiles * c * 4 <= ncu &&
-            (size_t)c * M * N * sizeof(float) <= epi.splitk_bytes) {
-          splits = c;
-          break;
-        }
+    int c = 1;
+    for (int d = 8; d >= 2; --d)
+      if (nkt % d == 0 && nkt / d >= 3) {
+        c = d;
+        break;
+      }
+    if (in_place && c > 1 && tiles * c <= vcap_device_cus() && (size_t)c * M * N * sizeof(float) <= epi.splitk_bytes)
+      splits = c;
   }
   hipLaunchKernelGGL((vcap_gemm_kernel<TIn, TOut, EPI>), dim3(tiles, splits), dim3(256), 0, s, (const TIn*)A, lda,
                      (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, epi);

@@ -18,6 +18,13 @@ token step (every step streams the 247 MB of weights once instead of once per ba
 independent in every decode kernel (per-row MFMA outputs, per-row processors), so a batch's ids
 are bit-identical whichever group it is decoded in (tests/test_gpu_bf16.py).  The price is latency:
 a batch waits for the next batch's encode before its decode starts.
+
+`enc_group` > 1 (a divisor of dec_group) encodes that many consecutive batches as one encode of
+enc_group * B videos: each submitted batch is copied into a staging buffer and the group's last
+submission launches the encode.  The ViT's N = 768 GEMMs (attn-proj, fc2) leave most of a
+second 256-tile round idle at B = 8 (297 tiles on 256 CUs); at 16 videos the rounds fill.  Every
+encode kernel computes each row independently of M (the CLS-tail split-K plan depends on K only),
+so a video's prefix - and its caption - is bit-identical whichever batch it is encoded in.
 """
 from __future__ import annotations
 
@@ -34,14 +41,21 @@ from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, _Workspa
 class CaptionPipeline:
     def __init__(self, encoder: HipViTEncoder, prefix: HipPrefix, decoder: HipGPT2Decoder, cfg: GenConfig,
                  batch: int, prompt_ids: Sequence[int], device, depth: int = 2, gather=None,
-                 reserve_cus: int = 0, dec_lanes: int = 1, confine_decode: bool = False, dec_group: int = 1):
+                 reserve_cus: int = 0, dec_lanes: int = 1, confine_decode: bool = False, dec_group: int = 1,
+                 enc_group: int = 1):
         self.enc, self.pre, self.dec, self.cfg = encoder, prefix, decoder, cfg
         self.prompt_ids = list(prompt_ids)
         self.device = torch.device(device)
-        if dec_lanes < 1 or dec_group < 1:
-            raise ValueError("dec_lanes and dec_group must be >= 1")
+        if dec_lanes < 1 or dec_group < 1 or enc_group < 1:
+            raise ValueError("dec_lanes, dec_group and enc_group must be >= 1")
+        if dec_group % enc_group:
+            raise ValueError(f"enc_group ({enc_group}) must divide dec_group ({dec_group})")
         self.lanes = int(dec_lanes)
         self.group = int(dec_group)
+        self.egroup = int(enc_group)
+        self._stage = None            # [enc_group * B, T, 3, H, W] staging buffer (enc_group > 1)
+        self._staged = 0              # batches copied into it since the last encode
+        self._pending_mid: List[torch.cuda.Event] = []
         self.batch = int(batch)
         depth = max(int(depth), self.lanes + 1)   # one slot being encoded + one per decoding lane
         self.depth = depth
@@ -100,7 +114,7 @@ class CaptionPipeline:
         Returns the submission slot for result() (k % (depth * dec_group)).  With dec_group > 1,
         t_end of a batch is recorded after its GROUP's decode; `gather(ids, first_k)` receives the
         group's [G*B, L] ids and the submission index of its first batch."""
-        G, B = self.group, self.batch
+        G, B, E = self.group, self.batch, self.egroup
         g, j = divmod(self.k, G)
         slot = g % self.depth
         with torch.cuda.stream(self.s_enc):
@@ -108,10 +122,17 @@ class CaptionPipeline:
                 self.s_enc.wait_event(self.dec_done[slot])   # buffers of group g-depth are free
             if t_start is not None:
                 t_start.record()
-            self.enc.encode(video, self.pre, out_prefix=self.group_prefix[slot][j * B:(j + 1) * B])
             if t_mid is not None:
-                t_mid.record()
-            self.enc_done[slot].record()
+                self._pending_mid.append(t_mid)
+            if E == 1:
+                self._encode(video, slot, j, 1)
+            else:
+                if self._stage is None or self._stage.shape[1:] != video.shape[1:] or self._stage.dtype != video.dtype:
+                    self._stage = torch.empty((E * B,) + tuple(video.shape[1:]), dtype=video.dtype, device=self.device)
+                self._stage[self._staged * B:(self._staged + 1) * B].copy_(video)
+                self._staged += 1
+                if self._staged == E:
+                    self._encode(self._stage, slot, j - E + 1, E)
         if t_end is not None:
             self._pending_end.append(t_end)
         self.k += 1
@@ -120,11 +141,25 @@ class CaptionPipeline:
             self._decode_group(g)
         return self.last_slot
 
+    def _encode(self, video: torch.Tensor, slot: int, j0: int, n: int) -> None:
+        """Encode n staged batches (on the encode stream) into submission positions j0.. of slot."""
+        B = self.batch
+        self.enc.encode(video[:n * B], self.pre, out_prefix=self.group_prefix[slot][j0 * B:(j0 + n) * B])
+        for ev in self._pending_mid:
+            ev.record()
+        self._pending_mid = []
+        self.enc_done[slot].record()
+        self._staged = 0
+
     def flush(self) -> None:
         """Decode a partially filled group now (its unfilled rows hold stale prefixes; their ids
         are ignored).  Called before waiting on results when k is not a multiple of dec_group."""
         if self.k % self.group:
             g = self.k // self.group
+            if self._staged:
+                with torch.cuda.stream(self.s_enc):
+                    j = self.k % self.group
+                    self._encode(self._stage, g % self.depth, j - self._staged, self._staged)
             self.k = (g + 1) * self.group
             self._decode_group(g)
 

@@ -66,8 +66,10 @@ def parse():
                     help="decodes in flight at once (own stream + workspace + graph each)")
     ap.add_argument("--dec-group", type=int, default=2,
                     help="consecutive batches decoded together as one decode of group*batch rows")
-    ap.add_argument("--enc-group", type=int, default=2,
-                    help="consecutive batches encoded together as one encode (divides --dec-group)")
+    ap.add_argument("--enc-group", type=int, default=0,
+                    help="consecutive batches encoded together as one encode (divides --dec-group); 0 = auto: "
+                         "2 while a batch holds <= 128 frames (the N = 768 GEMMs of one 8 x 16-frame batch fill "
+                         "1.16 rounds of 256 tiles), else 1")
     ap.add_argument("--confine-decode", action="store_true",
                     help="mask the decode streams to the reserved CUs (default: unmasked, high priority)")
     ap.add_argument("--gemm-policy", type=int, default=0, help="vcap_set_gemm_policy value for A/B runs (0 = auto)")
@@ -238,6 +240,8 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
+    if args.enc_group <= 0:
+        args.enc_group = 2 if args.batch * args.frames <= 128 and args.dec_group % 2 == 0 else 1
 
     va, ga = configs.vit_arch(args.vit), configs.gpt2_arch(args.gpt2)
     sd = weights.synthetic_state_dict(1, va, ga)

@@ -90,6 +90,135 @@ VCAP_DEV void lds_fence() { asm volatile("" ::: "memory"); }
 
 }  // namespace
 
+// Epilogue of a 256-row tile: wave (wr, wc) holds the 128 x 64 block at rows m0 + wr*128, columns
+// n0 + wc*64 as four 64 x 32 quadrants; lane holds C[m][n .. n+3] of each 16x16 MFMA tile
+// (m = .. + fr, n = .. + 4*fg).  Shared by the 256x256 and 256x128 kernels.
+template <typename TIn, typename TOut, int EPI>
+VCAP_DEV void epilogue256(const f32x4 (&acc)[2][2][4][2], int m0, int n0, int wr, int wc, int lane, int M, int N,
+                          TOut* C, long ldc, const GemmEpi& epi) {
+  const int fr = lane & 15, fg = lane >> 4;
+  if constexpr (EPI == 4) {
+    // bias + GELU, re-quantised to MXFP8 for the next GEMM: the 32-column block
+    // n0 + wc*64 + qn*32 of row m lives in this lane (j = 0, 1) and the lanes fg = 0..3 of the
+    // same fr, so its max |x| is a 2-step permlane reduction.
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn) {
+        const int nb = n0 + wc * 64 + qn * 32;
+        f32x4 bias[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int n = min(nb + j * 16 + fg * 4, N - 4);
+          bias[j] = *reinterpret_cast<const f32x4*>(epi.bias + n);
+        }
+        // rows i and i+1 (16 apart) at a time: after quantisation the 4 lanes of a row hold 4
+        // fp8 of each 16-column half; a 4x4 lane-group transpose gives every lane 16 contiguous
+        // bytes (group 0: row i cols 0-15, 1: row i cols 16-31, 2 / 3: row i+1), one dwordx4
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          uint32_t x[4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int m = m0 + wr * 128 + qm * 64 + (i + h) * 16 + fr;
+            f32x4 v[2];
+            float amax = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              v[j] = gelu_tanh4(acc[qm][qn][i + h][j] + bias[j]);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fabsf(v[j][e]));
+            }
+            amax = rows_max(amax);
+            const int sbyte = mx_scale_byte(amax);
+            const float inv = mx_inv_scale(sbyte);
+            const f32x4 q0 = v[0] * inv, q1 = v[1] * inv;
+            x[2 * h] = pack_fp8x4(q0.x, q0.y, q0.z, q0.w);
+            x[2 * h + 1] = pack_fp8x4(q1.x, q1.y, q1.z, q1.w);
+            if (fg == 0 && m < M && nb < N) epi.c_scale[mx_scale_index(m, nb, (M + 255) >> 8)] = (uint8_t)sbyte;
+          }
+          transpose4_groups(x);
+          const int ms = m0 + wr * 128 + qm * 64 + (i + (fg >> 1)) * 16 + fr;
+          if (ms < M && nb < N)
+            out_store(reinterpret_cast<u32x4*>((uint8_t*)C + (long)ms * ldc + nb + (fg & 1) * 16),
+                      (u32x4){x[0], x[1], x[2], x[3]});
+        }
+      }
+  } else if (sizeof(TOut) == 2 && (EPI == 0 || EPI == 1) && (N & 31) == 0 && (ldc & 7) == 0 &&
+             ((uintptr_t)C & 15) == 0) {
+    // bf16 out, 16-byte stores: lanes fg and fg ^ 1 (lane ^ 16) trade halves so the even lane
+    // holds columns [8k, 8k+8) of the j = 0 tile and the odd lane [16+8k, +8) of the j = 1 tile
+    // (k = fg >> 1); one dwordx4 store per row instead of two dwordx2 (the epilogue's store
+    // issue, not HBM bandwidth, is what the row-per-lane dwordx2 pattern pays for)
+    const bool odd = (lane & 16) != 0;
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn) {
+        const int nb = n0 + wc * 64 + qn * 32;
+        f32x4 bias[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bias[j] = epi.bias ? *reinterpret_cast<const f32x4*>(epi.bias + min(nb + j * 16 + fg * 4, N - 4))
+                             : (f32x4){0.f, 0.f, 0.f, 0.f};
+        const int col = nb + (odd ? 12 + 4 * fg : 4 * fg);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wr * 128 + qm * 64 + i * 16 + fr;
+          uint32_t p[2][2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            f32x4 v = acc[qm][qn][i][j] + bias[j];
+            if constexpr (EPI == 1) v = gelu_tanh4(v);
+            p[j][0] = pack_bf2(v.x, v.y);
+            p[j][1] = pack_bf2(v.z, v.w);
+          }
+          const uint32_t r0 = (uint32_t)xor16_i((int)(odd ? p[0][0] : p[1][0]));
+          const uint32_t r1 = (uint32_t)xor16_i((int)(odd ? p[0][1] : p[1][1]));
+          const u32x4 o = odd ? (u32x4){r0, r1, p[1][0], p[1][1]} : (u32x4){p[0][0], p[0][1], r0, r1};
+          if (m < M && nb < N) out_store(reinterpret_cast<u32x4*>(C + (long)m * ldc + col), o);
+        }
+      }
+  } else {
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wc * 64 + qn * 32 + j * 16 + fg * 4;
+        if (n >= N) continue;
+        const f32x4 bias = epi.bias ? *reinterpret_cast<const f32x4*>(epi.bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wr * 128 + qm * 64 + i * 16 + fr;
+          if (m >= M) continue;
+          f32x4 v = acc[qm][qn][i][j] + bias;
+          long orow = m;
+          if constexpr (EPI == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+          } else if constexpr (EPI == 2) {
+            v += *reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n);
+          } else if constexpr (EPI == 3) {
+            if (epi.act == 1)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+            orow = epi.G ? (long)(m / epi.G) * epi.Gs + epi.goff + (m % epi.G) : (long)m;
+            if (epi.res_mode == 1) v += *reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n);
+            else if (epi.res_mode == 2)
+              v += *reinterpret_cast<const f32x4*>(epi.res + (long)((m % epi.G) + epi.roff) * epi.ldr + n);
+          }
+          if constexpr (sizeof(TOut) == 2) {
+            out_store(reinterpret_cast<u32x2*>(C + orow * ldc + n), (u32x2){pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)});
+          } else {
+            out_store(reinterpret_cast<f32x4*>(C + orow * ldc + n), v);
+          }
+        }
+      }
+  }
+}
+
 template <typename TIn, typename TOut, int EPI>
 __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict__ A, long lda,
                                                            const TIn* __restrict__ W, long ldw, TOut* C, long ldc,
@@ -313,127 +442,7 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
   if (wr == 0) __builtin_amdgcn_s_barrier();
   if constexpr (MX) mfma_mx_drain();
 
-  // ---- epilogue: lane holds C[m][n .. n+3] of each 16x16 tile (m = .. + fr, n = .. + 4*fg)
-  if constexpr (EPI == 4) {
-    // bias + GELU, re-quantised to MXFP8 for the next GEMM: the 32-column block
-    // n0 + wc*64 + qn*32 of row m lives in this lane (j = 0, 1) and the lanes fg = 0..3 of the
-    // same fr, so its max |x| is a 2-step permlane reduction.
-#pragma unroll
-    for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-      for (int qn = 0; qn < 2; ++qn) {
-        const int nb = n0 + wc * 64 + qn * 32;
-        f32x4 bias[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int n = min(nb + j * 16 + fg * 4, N - 4);
-          bias[j] = *reinterpret_cast<const f32x4*>(epi.bias + n);
-        }
-        // rows i and i+1 (16 apart) at a time: after quantisation the 4 lanes of a row hold 4
-        // fp8 of each 16-column half; a 4x4 lane-group transpose gives every lane 16 contiguous
-        // bytes (group 0: row i cols 0-15, 1: row i cols 16-31, 2 / 3: row i+1), one dwordx4
-#pragma unroll
-        for (int i = 0; i < 4; i += 2) {
-          uint32_t x[4];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int m = m0 + wr * 128 + qm * 64 + (i + h) * 16 + fr;
-            f32x4 v[2];
-            float amax = 0.f;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              v[j] = gelu_tanh4(acc[qm][qn][i + h][j] + bias[j]);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fabsf(v[j][e]));
-            }
-            amax = rows_max(amax);
-            const int sbyte = mx_scale_byte(amax);
-            const float inv = mx_inv_scale(sbyte);
-            const f32x4 q0 = v[0] * inv, q1 = v[1] * inv;
-            x[2 * h] = pack_fp8x4(q0.x, q0.y, q0.z, q0.w);
-            x[2 * h + 1] = pack_fp8x4(q1.x, q1.y, q1.z, q1.w);
-            if (fg == 0 && m < M && nb < N) epi.c_scale[mx_scale_index(m, nb, (M + 255) >> 8)] = (uint8_t)sbyte;
-          }
-          transpose4_groups(x);
-          const int ms = m0 + wr * 128 + qm * 64 + (i + (fg >> 1)) * 16 + fr;
-          if (ms < M && nb < N)
-            out_store(reinterpret_cast<u32x4*>((uint8_t*)C + (long)ms * ldc + nb + (fg & 1) * 16),
-                      (u32x4){x[0], x[1], x[2], x[3]});
-        }
-      }
-  } else if (sizeof(TOut) == 2 && (EPI == 0 || EPI == 1) && (N & 31) == 0 && (ldc & 7) == 0 &&
-             ((uintptr_t)C & 15) == 0) {
-    // bf16 out, 16-byte stores: lanes fg and fg ^ 1 (lane ^ 16) trade halves so the even lane
-    // holds columns [8k, 8k+8) of the j = 0 tile and the odd lane [16+8k, +8) of the j = 1 tile
-    // (k = fg >> 1); one dwordx4 store per row instead of two dwordx2 (the epilogue's store
-    // issue, not HBM bandwidth, is what the row-per-lane dwordx2 pattern pays for)
-    const bool odd = (lane & 16) != 0;
-#pragma unroll
-    for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-      for (int qn = 0; qn < 2; ++qn) {
-        const int nb = n0 + wc * 64 + qn * 32;
-        f32x4 bias[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          bias[j] = epi.bias ? *reinterpret_cast<const f32x4*>(epi.bias + min(nb + j * 16 + fg * 4, N - 4))
-                             : (f32x4){0.f, 0.f, 0.f, 0.f};
-        const int col = nb + (odd ? 12 + 4 * fg : 4 * fg);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0 + wr * 128 + qm * 64 + i * 16 + fr;
-          uint32_t p[2][2];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            f32x4 v = acc[qm][qn][i][j] + bias[j];
-            if constexpr (EPI == 1) v = gelu_tanh4(v);
-            p[j][0] = pack_bf2(v.x, v.y);
-            p[j][1] = pack_bf2(v.z, v.w);
-          }
-          const uint32_t r0 = (uint32_t)xor16_i((int)(odd ? p[0][0] : p[1][0]));
-          const uint32_t r1 = (uint32_t)xor16_i((int)(odd ? p[0][1] : p[1][1]));
-          const u32x4 o = odd ? (u32x4){r0, r1, p[1][0], p[1][1]} : (u32x4){p[0][0], p[0][1], r0, r1};
-          if (m < M && nb < N) out_store(reinterpret_cast<u32x4*>(C + (long)m * ldc + col), o);
-        }
-      }
-  } else {
-#pragma unroll
-  for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-    for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wc * 64 + qn * 32 + j * 16 + fg * 4;
-        if (n >= N) continue;
-        const f32x4 bias = epi.bias ? *reinterpret_cast<const f32x4*>(epi.bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0 + wr * 128 + qm * 64 + i * 16 + fr;
-          if (m >= M) continue;
-          f32x4 v = acc[qm][qn][i][j] + bias;
-          long orow = m;
-          if constexpr (EPI == 1) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
-          } else if constexpr (EPI == 2) {
-            v += *reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n);
-          } else if constexpr (EPI == 3) {
-            if (epi.act == 1)
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
-            orow = epi.G ? (long)(m / epi.G) * epi.Gs + epi.goff + (m % epi.G) : (long)m;
-            if (epi.res_mode == 1) v += *reinterpret_cast<const f32x4*>(epi.res + orow * epi.ldr + n);
-            else if (epi.res_mode == 2)
-              v += *reinterpret_cast<const f32x4*>(epi.res + (long)((m % epi.G) + epi.roff) * epi.ldr + n);
-          }
-          if constexpr (sizeof(TOut) == 2) {
-            out_store(reinterpret_cast<u32x2*>(C + orow * ldc + n), (u32x2){pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)});
-          } else {
-            out_store(reinterpret_cast<f32x4*>(C + orow * ldc + n), v);
-          }
-        }
-      }
-  }
+  epilogue256<TIn, TOut, EPI>(acc, m0, n0, wr, wc, lane, M, N, C, ldc, epi);
 }
 
 template <typename TIn, typename TOut, int EPI>

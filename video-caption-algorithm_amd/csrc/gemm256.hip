@@ -92,7 +92,7 @@ VCAP_DEV void lds_fence() { asm volatile("" ::: "memory"); }
 
 // Epilogue of a 256-row tile: wave (wr, wc) holds the 128 x 64 block at rows m0 + wr*128, columns
 // n0 + wc*64 as four 64 x 32 quadrants; lane holds C[m][n .. n+3] of each 16x16 MFMA tile
-// (m = .. + fr, n = .. + 4*fg).  Shared by the 256x256 and 256x128 kernels.
+// (m = .. + fr, n = .. + 4*fg).
 template <typename TIn, typename TOut, int EPI>
 VCAP_DEV void epilogue256(const f32x4 (&acc)[2][2][4][2], int m0, int n0, int wr, int wc, int lane, int M, int N,
                           TOut* C, long ldc, const GemmEpi& epi) {

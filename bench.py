@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="no encode/decode overlap (each step's decode finishes before the next encode starts)")
-    ap.add_argument("--reserve-cus", type=int, default=0,
+    ap.add_argument("--reserve-cus", type=int, default=32,
                     help="CUs the encode stream leaves to the decode stream (CU-masked stream; 0 = none)")
     ap.add_argument("--decode-blocks", type=int, default=96,
                     help="cap the decode GEMV grids near this many workgroups (0 = whole-chip grids)")

@@ -501,6 +501,114 @@ __global__ __launch_bounds__(256) void vcap_decode_attention_anc_kernel(const T*
   }
 }
 
+// Short-context variant (ctx = past + 1 <= 64, every configs[3] beam step): two memory round trips
+// per wave instead of two per 8-key group - (1) the query element and the ancestry entry of key
+// `lane`, (2) that key's K row and all 8 V-row chunks this lane accumulates, issued together.
+// Arithmetic in the same order as the general kernel above (bit-identical outputs).
+template <typename T>
+__global__ __launch_bounds__(256) void vcap_decode_attention_anc64_kernel(const T* __restrict__ q,
+                                                                          const T* __restrict__ kc,
+                                                                          const T* __restrict__ vc,
+                                                                          const int* __restrict__ anc, int anc_ld,
+                                                                          int maxp, T* __restrict__ out, int M,
+                                                                          int H, int past) {
+  constexpr int E8 = Frag<T>::kElems;
+  constexpr int VC = sizeof(T) == 2 ? 1 : 2;  // 16-byte V chunks per 8 dims
+  __shared__ float s_q[4][64];
+  __shared__ float s_p[4][64];
+  __shared__ int s_a[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int item = blockIdx.x * 4 + wave;
+  if (item >= M * H) return;
+  const int m = item / H, h = item - m * H;
+  const int E = H * 64;
+  const int ctx = past + 1;
+  const int* arow = anc + (long)m * anc_ld;
+  auto row_of = [&](const T* pool, int j, int phys) {
+    return pool + (((long)(phys * maxp + (j >> 4)) * H + h) * 16 + (j & 15)) * 64;
+  };
+  // ---- round trip 1
+  const int jk = min(lane, ctx - 1);
+  const float qv = Num<T>::to_f(q[(long)m * E + h * 64 + lane]);
+  const int ak = arow[jk];
+  s_q[wave][lane] = qv;
+  s_a[wave][lane] = ak;
+  __builtin_amdgcn_wave_barrier();
+  // ---- round trip 2: K row of key `lane`, V chunks of keys kg, kg + 8, ...
+  const int kg = lane >> 3, d8 = (lane & 7) * 8;
+  const T* krow = row_of(kc, jk, ak);
+  u32x4 kv[64 / E8];
+#pragma unroll
+  for (int c = 0; c < 64 / E8; ++c) kv[c] = *reinterpret_cast<const u32x4*>(krow + c * E8);
+  u32x4 vv[8][VC];
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int j = min(it * 8 + kg, ctx - 1);
+    const T* vrow = row_of(vc, j, s_a[wave][j]) + d8;
+#pragma unroll
+    for (int c = 0; c < VC; ++c) vv[it][c] = *reinterpret_cast<const u32x4*>(vrow + c * 4);
+  }
+  float sc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 64 / E8; ++c) {
+    const T* ke = reinterpret_cast<const T*>(&kv[c]);
+#pragma unroll
+    for (int e = 0; e < E8; ++e) sc += s_q[wave][c * E8 + e] * Num<T>::to_f(ke[e]);
+  }
+  sc *= 0.125f;
+  float mx = -INFINITY;
+  if (lane < ctx) {
+    s_p[wave][lane] = sc;
+    mx = sc;
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  if (lane < ctx) {
+    const float p = __expf(s_p[wave][lane] - mx);
+    s_p[wave][lane] = p;
+    sum = p;
+  }
+  sum = wave_sum(sum);
+  __builtin_amdgcn_wave_barrier();
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = 0.f;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int jj = it * 8 + kg;
+    const float p = jj < ctx ? s_p[wave][min(jj, ctx - 1)] : 0.f;
+    if constexpr (sizeof(T) == 2) {
+      const unsigned w4[4] = {vv[it][0].x, vv[it][0].y, vv[it][0].z, vv[it][0].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[2 * e] += p * bf2f((bf16_t)(w4[e] & 0xffff));
+        o[2 * e + 1] += p * bf2f((bf16_t)(w4[e] >> 16));
+      }
+    } else {
+      const f32x4 v0 = __builtin_bit_cast(f32x4, vv[it][0]), v1 = __builtin_bit_cast(f32x4, vv[it][1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] += p * v0[e];
+        o[4 + e] += p * v1[e];
+      }
+    }
+  }
+  #pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = rows_sum(o[e] + dpp_f<0x128>(o[e]));
+  if (kg == 0) {
+    const float inv = 1.0f / sum;
+    T* orow = out + (long)m * E + h * 64 + d8;
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<u32x4*>(orow) =
+          (u32x4){pack_bf2(o[0] * inv, o[1] * inv), pack_bf2(o[2] * inv, o[3] * inv),
+                  pack_bf2(o[4] * inv, o[5] * inv), pack_bf2(o[6] * inv, o[7] * inv)};
+    } else {
+      *reinterpret_cast<f32x4*>(orow) = (f32x4){o[0], o[1], o[2], o[3]} * inv;
+      *reinterpret_cast<f32x4*>(orow + 4) = (f32x4){o[4], o[5], o[6], o[7]} * inv;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 hipError_t vcap_beam_init_dispatch(const BeamState& st, int B, int nb, int L, int S0, int anc_ld, int eos,
                                    hipStream_t s) {
@@ -552,6 +660,15 @@ hipError_t vcap_decode_attention_anc_dispatch(int dt, const void* q, const void*
                                               hipStream_t s) {
   if (past + 1 > 1024 || past + 1 > anc_ld) return hipErrorInvalidValue;
   const dim3 grid((M * H + 3) / 4), block(256);
+  if (past + 1 <= 64) {
+    if (dt == VCAP_DT_BF16)
+      hipLaunchKernelGGL((vcap_decode_attention_anc64_kernel<bf16_t>), grid, block, 0, s, (const bf16_t*)q,
+                         (const bf16_t*)kc, (const bf16_t*)vc, anc, anc_ld, maxp, (bf16_t*)out, M, H, past);
+    else
+      hipLaunchKernelGGL((vcap_decode_attention_anc64_kernel<float>), grid, block, 0, s, (const float*)q,
+                         (const float*)kc, (const float*)vc, anc, anc_ld, maxp, (float*)out, M, H, past);
+    return hipGetLastError();
+  }
   if (dt == VCAP_DT_BF16)
     hipLaunchKernelGGL((vcap_decode_attention_anc_kernel<bf16_t>), grid, block, 0, s, (const bf16_t*)q,
                        (const bf16_t*)kc, (const bf16_t*)vc, anc, anc_ld, maxp, (bf16_t*)out, M, H, past);

@@ -232,6 +232,8 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
     }
   }
 
+  if constexpr (PRO == PRO_LN || NSL * (NTB + MT) < 64)
+    asm volatile("" ::: "memory");  // the activation loads issue (and retire) before the weights
   // ---- 2) weights
   u32x4 wf[NSL][NTB];
 #pragma unroll
@@ -247,12 +249,29 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   for (int q = 0; q < NE; ++q) {
     const int m = m0 + (q / NTB) * 16 + (tid >> 4), n = n0 + (q % NTB) * 16 + (tid & 15);
     const int mc = min(m, M - 1), nc = min(n, N - 1);
-    pre_bias[q] = a.bias ? a.bias[nc] : 0.f;
+    // unconditional load (from a valid address when there is no bias), then a select: a load
+    // guarded by the runtime `a.bias` test compiled to a branch + vmcnt(0) that waited for the
+    // whole weight stream before the LayerNorm / A-fragment work could start
+    const float bl = *(a.bias ? a.bias + nc : (const float*)a.x);
+    pre_bias[q] = a.bias ? bl : 0.f;
     pre_res[q] = 0.f;
     if constexpr (EPI == EPI_RESID) pre_res[q] = ((const float*)a.out)[(long)mc * a.ldo + nc];
   }
   ProcToks<EPI == EPI_LOGITS ? MT : 1> toks;
   if constexpr (EPI == EPI_LOGITS) toks.load(a, m0);
+  // Issue order fence: every load above is issued before any of the work below.  The empty asm
+  // statements take the first-consumed operands as in/out registers and clobber memory, so no
+  // load sinks below them and no LayerNorm arithmetic / MFMA chain is hoisted above them (the
+  // scheduler otherwise sank the weight stream below the LayerNorm, or issued it ~8 loads at a
+  // time between the MFMAs); the waits they imply are for the oldest loads only.
+  if constexpr (PRO == PRO_LN) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int c = 0; c < KC; ++c) asm volatile("" : "+v"(xv[r][c])::"memory");
+  } else if constexpr (NSL * (NTB + MT) < 64) {  // (at the 64-fragment budget: let the compiler stream)
+    asm volatile("" : "+v"(af[0][0])::"memory");
+  }
 
   // ---- LayerNorm in registers -> swizzled LDS tile (waits only for step 1's loads)
   if constexpr (PRO == PRO_LN) {
@@ -436,7 +455,11 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
   for (int q = 0; q < NE; ++q) {
     const int m = m0 + (q / NTB) * 16 + (tid >> 4), n = n0 + (q % NTB) * 16 + (tid & 15);
     const int mc = min(m, M - 1), nc = min(n, N - 1);
-    pre_bias[q] = a.bias ? a.bias[nc] : 0.f;
+    // unconditional load (from a valid address when there is no bias), then a select: a load
+    // guarded by the runtime `a.bias` test compiled to a branch + vmcnt(0) that waited for the
+    // whole weight stream before the LayerNorm / A-fragment work could start
+    const float bl = *(a.bias ? a.bias + nc : (const float*)a.x);
+    pre_bias[q] = a.bias ? bl : 0.f;
     pre_res[q] = 0.f;
     if constexpr (EPI == EPI_RESID) pre_res[q] = ((const float*)a.out)[(long)mc * a.ldo + nc];
   }
@@ -665,10 +688,28 @@ __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
   __shared__ int s_h[1024];
   __shared__ int s_tok, s_nb;
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int t = tid; t < step; t += 256) s_h[t] = hist[m * hist_ld + t];
+  // every load of the first phase issued at once (clamped addresses, selects after): the history,
+  // the argmax partials (nblk <= 1024) and the row's finished flag
+  constexpr int HP = 4, PP = 4;
+  int hv[HP], pi[PP];
+  float pv[PP];
+#pragma unroll
+  for (int q = 0; q < HP; ++q) hv[q] = hist[m * hist_ld + min(tid + q * 256, hist_ld - 1)];
+#pragma unroll
+  for (int q = 0; q < PP; ++q) {
+    const int b = min(tid + q * 256, nblk - 1);
+    pv[q] = part_val[(long)m * nblk + b];
+    pi[q] = part_idx[(long)m * nblk + b];
+  }
+  const int fin = finished[m];
+#pragma unroll
+  for (int q = 0; q < HP; ++q)
+    if (tid + q * 256 < step) s_h[tid + q * 256] = hv[q];
   float bv = -INFINITY;
   int bi = 0x7fffffff;
-  for (int b = tid; b < nblk; b += 256) argmax_take(bv, bi, part_val[(long)m * nblk + b], part_idx[(long)m * nblk + b]);
+#pragma unroll
+  for (int q = 0; q < PP; ++q)
+    if (tid + q * 256 < nblk) argmax_take(bv, bi, pv[q], pi[q]);
   wave_argmax(bv, bi);
   if (lane == 0) {
     sv[wave] = bv;
@@ -679,7 +720,7 @@ __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
     for (int w = 1; w < 4; ++w) argmax_take(bv, bi, sv[w], si[w]);
     int tok = bi;
     tok = tok < 0 ? 0 : (tok >= vocab ? vocab - 1 : tok);  // all -inf row (cannot happen with finite logits)
-    if (finished[m]) tok = pad;
+    if (fin) tok = pad;
     out_ids[(long)m * out_ld + step] = tok;
     hist[m * hist_ld + step] = tok;
     s_h[step] = tok;
@@ -985,7 +1026,7 @@ hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const in
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,
                                          const float* wpe, float* h, int E, int pos_next, int vocab, hipStream_t s) {
-  if (hist_ld > 1024) return hipErrorInvalidValue;
+  if (hist_ld > 1024 || nblk < 1 || nblk > 1024 || step >= hist_ld) return hipErrorInvalidValue;
   if (dt == VCAP_DT_BF16)
     hipLaunchKernelGGL((vcap_decode_finalize_kernel<bf16_t>), dim3(B), dim3(256), 0, s, part_val, part_idx, nblk,
                        step, finished, hist, hist_ld, banned, nbanned, ngram, eos, pad, out_ids, out_ld,

@@ -58,8 +58,9 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="no encode/decode overlap (each step's decode finishes before the next encode starts)")
-    ap.add_argument("--reserve-cus", type=int, default=32,
-                    help="CUs the encode stream leaves to the decode stream (CU-masked stream; 0 = none)")
+    ap.add_argument("--reserve-cus", type=int, default=-1,
+                    help="CUs the encode stream leaves to the decode stream (CU-masked stream; 0 = none; "
+                         "-1 = auto: 32 with two-batch encodes, else 0 - profiles/r02_decode_experiments.txt)")
     ap.add_argument("--decode-blocks", type=int, default=96,
                     help="cap the decode GEMV grids near this many workgroups (0 = whole-chip grids)")
     ap.add_argument("--dec-lanes", type=int, default=2,
@@ -242,6 +243,8 @@ def main():
     torch.cuda.set_device(dev)
     if args.enc_group <= 0:
         args.enc_group = 2 if args.batch * args.frames <= 128 and args.dec_group % 2 == 0 else 1
+    if args.reserve_cus < 0:
+        args.reserve_cus = 32 if args.enc_group == 2 else 0
 
     va, ga = configs.vit_arch(args.vit), configs.gpt2_arch(args.gpt2)
     sd = weights.synthetic_state_dict(1, va, ga)

@@ -1,4 +1,4 @@
-"""Decode step time (B=8, hipGraph) when the decode stream may use only R CUs (CU-masked stream),
+"""Decode step time (B rows, env B=8 default, hipGraph) when the decode stream may use only R CUs (CU-masked stream),
 with the GPU otherwise idle, and with an encode loop running on the complementary CUs.
 Separates 'fewer CUs' from 'contention' in the overlapped pipeline."""
 import ctypes as C
@@ -21,7 +21,9 @@ enc = HipViTEncoder(sd, va, "bf16", dev)
 pre = HipPrefix(sd, ga.n_embd, device=dev)
 dec = HipGPT2Decoder(sd, ga, "bf16", dev)
 video = torch.from_numpy(prng.imagenet_frames(1000, (8, 16, 3, 224, 224))).to(dev)
-prefix = torch.randn(8, 4, 768, device=dev) * 0.1
+import os
+B = int(os.environ.get("B", "8"))
+prefix = torch.randn(B, 4, 768, device=dev) * 0.1
 lib = N.lib()
 
 
@@ -47,8 +49,8 @@ def step_us(s, cap):
     return (res[24] - res[1]) / 23 * 1e6, res[24] * 1e3
 
 
-for R in (256, 128, 64, 48, 32):
-    for cap in (0, 2 * R):
+for R in [int(x) for x in os.environ.get("RS", "256,128,64,48,32").split(",")]:
+    for cap in [int(c) * R if c != "0" else 0 for c in os.environ.get("CAPS", "0,2").split(",")]:
         s_dec = masked(256 - R) if R < 256 else torch.cuda.Stream(dev)
         alone = step_us(s_dec, cap)
         # the same with an encode loop on the other CUs

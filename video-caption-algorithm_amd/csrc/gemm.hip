@@ -123,6 +123,23 @@ __global__ __launch_bounds__(256) void vcap_gemm_kernel(const TIn* __restrict__ 
 
   // epilogue: lane holds row fr, columns 4*fg .. 4*fg+3 of each 16x16 tile
   const bool vec = (N & 3) == 0 && (ldc & 3) == 0 && (!epi.res || (epi.ldr & 3) == 0);
+  // in-place residual (EPI 2): every residual row of the wave is loaded before the first store
+  // (load / add / store per element serialised 16 HBM round trips: the loads cannot pass the
+  // previous store to the same pointer, and the in-order vmcnt waits for that store too)
+  f32x4 rpre[4][4];
+  const bool pre = EPI == 2 && vec && !split;
+  if constexpr (EPI == 2) {
+    if (pre) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = min(m0 + wm * 64 + i * 16 + fr, M - 1);
+          const int nb = min(n0 + wn * 64 + j * 16 + 4 * fg, N - 4);
+          rpre[i][j] = *reinterpret_cast<const f32x4*>(epi.res + (long)m * epi.ldr + nb);
+        }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int nb = n0 + wn * 64 + j * 16 + 4 * fg;
@@ -158,7 +175,10 @@ __global__ __launch_bounds__(256) void vcap_gemm_kernel(const TIn* __restrict__ 
         else if (epi.res_mode == 2) rr = epi.res + (long)((m % epi.G) + epi.roff) * epi.ldr + nb;
       }
       if (vec && nb + 3 < N) {
-        if (rr) {
+        if (pre) {
+          const f32x4 r = rpre[i][j];
+          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+        } else if (rr) {
           const f32x4 r = *reinterpret_cast<const f32x4*>(rr);
           v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
         }

@@ -220,10 +220,26 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
 #pragma unroll
     for (int r = 0; r < 4; ++r) st[kt][r] = r < lim ? st[kt][r] : -INFINITY;
   }
-  // row max: two v_max3 per key tile; exp2 argument and row sum as packed f32 pairs
-  float mx = -INFINITY;
+  // row max: two v_max3 per key tile
+  float mx;
+#ifdef VCAP_ATTN_SERIAL_MAX
+  mx = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < KE; ++kt) mx = max3f(max3f(mx, st[kt][0], st[kt][1]), st[kt][2], st[kt][3]);
+#else
+  {
+    // four independent v_max3 chains (one per accumulator element) instead of one 26-deep
+    // dependent chain; the same instruction count
+    float m4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      m4[r] = st[0][r];
+#pragma unroll
+      for (int kt = 1; kt < KE; kt += 2) m4[r] = kt + 1 < KE ? max3f(m4[r], st[kt][r], st[kt + 1][r]) : fmaxf(m4[r], st[kt][r]);
+    }
+    mx = fmaxf(max3f(m4[0], m4[1], m4[2]), m4[3]);
+  }
+#endif
   mx = rows_max(mx);
 #ifdef VCAP_ATTN_PACKED_SOFTMAX
   const f32x2 c2v = (f32x2){c2, c2}, nmx = (f32x2){-mx * c2, -mx * c2};
@@ -239,7 +255,7 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
       sum2 += p;
     }
   const float sum = rows_sum(sum2.x + sum2.y);
-#else
+#elif defined(VCAP_ATTN_VALU_SUM)
   const float mxc = mx * c2;
   float sum = 0.f;
 #pragma unroll
@@ -251,12 +267,26 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
       sum += p;
     }
   sum = rows_sum(sum);
+#else
+  // the row sum comes out of the PV MFMAs below (a ones operand beside V), so the softmax here
+  // is one FMA + one exp per score
+  const float mxc = mx * c2;
+#pragma unroll
+  for (int kt = 0; kt < KE; ++kt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], c2, -mxc));
 #endif
 
   // O^T[d][q] = sum_key V[key][d] P^T[key][q]; k element j of lane group g <-> key
   // 32c + 4g + j (j < 4) / 32c + 16 + 4g + (j - 4), matching the P^T fragment below
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#if !defined(VCAP_ATTN_VALU_SUM) && !defined(VCAP_ATTN_PACKED_SOFTMAX)
+  // S[q] = sum_key 1 * P^T[key][q]: every output row of this MFMA is the sum of the bf16 P the
+  // PV products use (lane (fr, fg) gets query fr's sum in each element)
+  f32x4 osum = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const u32x4 ones = (u32x4){0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+#endif
   const int qr = fr >> 2, p4 = fr & 3;
 #pragma unroll
   for (int c = 0; c < KT / 2; ++c) {
@@ -271,8 +301,14 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
       const u32x2 hi = tr_read(Vs + r1 * 128 + ((ch ^ (r1 & 7)) << 4) + 8 * (p4 & 1));
       o[dt] = mfma_frag((u32x4){lo.x, lo.y, hi.x, hi.y}, pf, o[dt], (bf16_t*)nullptr);
     }
+#if !defined(VCAP_ATTN_VALU_SUM) && !defined(VCAP_ATTN_PACKED_SOFTMAX)
+    osum = mfma_frag(ones, pf, osum, (bf16_t*)nullptr);
+#endif
   }
-  inv = 1.0f / sum;
+#if !defined(VCAP_ATTN_VALU_SUM) && !defined(VCAP_ATTN_PACKED_SOFTMAX)
+  const float sum = osum[0];
+#endif
+  inv = __builtin_amdgcn_rcpf(sum);
 }
 
 // A query tile's output, packed for its stores: bf16 -> two dwordx4 per lane (lane pair exchange),

@@ -24,6 +24,12 @@ M = int(sys.argv[1]) if len(sys.argv) > 1 else 50432
 dev = torch.device("cuda:0")
 lib = N.lib()
 s = torch.cuda.current_stream().cuda_stream
+import os
+RESERVE = int(os.environ.get("RESERVE", "0"))  # run on a stream CU-masked off RESERVE CUs (the bench's encode stream)
+if RESERVE:
+    h = C.c_void_p()
+    N.check(lib.vcap_stream_create_cu_reserved(RESERVE, C.byref(h)), "stream")
+    s = h.value
 g = torch.Generator(device=dev).manual_seed(0)
 
 
@@ -86,6 +92,12 @@ for name, (n, k, f32, act, res) in shapes.items():
         for a, b2 in zip(lst, lst[1:]):
             gaps_done.append(ent[b2] - don[a])
             gaps_iss.append(ent[b2] - iss[a])
+    xcc = (st[:, 5] >> 32).astype(np.int64)
+    bids = np.arange(tiles)
+    for mod in (7, 8):
+        same = np.mean([len(set(xcc[bids % mod == r].tolist())) == 1 for r in range(mod)])
+        print(f"   bid % {mod}: fraction of residues whose workgroups all ran on one XCC: {same:.2f}")
+    print(f"   XCCs used: {sorted(set(xcc.tolist()))}; first 16 bids -> XCC {xcc[:16].tolist()}")
     if gaps_done:
         print(f"   CUs seen {ncu}; gap next-entry minus prev stores-done: median {statistics.median(gaps_done):.2f} us; "
               f"minus prev epilogue-issued: median {statistics.median(gaps_iss):.2f} us")

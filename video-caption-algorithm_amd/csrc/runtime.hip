@@ -534,8 +534,9 @@ int vcap_stream_create_cu_reserved(int reserve_cus, void** stream) {
   int ncu = 0;
   VCAP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "cu count");
   if (reserve_cus >= ncu) return fail(VCAP_E_ARG, "cannot reserve every CU");
-  // Consecutive mask bits fill one XCD (32 CUs) before the next (measured: tools/decode_xcd_sweep.py),
-  // so clearing the first `reserve_cus` bits hands whole XCDs - and their L2s - to the other streams.
+  // Clearing the first `reserve_cus` mask bits: with 32 cleared, the stream's workgroups still land on
+  // all 8 XCCs and block id % 8 still picks one XCC, so the GEMMs' XCD-aware tile remap
+  // holds (tools/gemm_stamps.py with RESERVE=32, profiles/r02_encode_alone.txt).
   std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
   for (int c = reserve_cus; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
   hipStream_t s = nullptr;

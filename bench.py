@@ -43,7 +43,10 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    # 60 batches: the timed region starts with an empty pipeline and ends with the last decode
+    # running alone (~9 ms), so short runs under-report the steady-state rate (30 -> 60 steps:
+    # 1207 -> 1230 captions/s, profiles/r02_pipeline_sweeps.txt); 60 steps take ~0.4 s
+    ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--batch", type=int, default=8, help="videos per GPU")
     ap.add_argument("--frames", type=int, default=16)

@@ -172,6 +172,14 @@ __global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __rest
 // operand that overwrites the source-C registers of an MFMA still in flight.)
 VCAP_DEV float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 
+// minimum waves per SIMD the per-(frame, head) kernel is compiled for at the ViT-B/16 shape (KT = 14).
+// 1 = no register constraint (90 VGPRs, two 8-wave workgroups per CU).  6 would fit three workgroups
+// per CU beside the 53 KiB K / V images (80 VGPRs, the second tile's Q fragments in scratch) and
+// measured 5-10 % slower (profiles/r02_attention_sum_mfma_ab.txt).
+#ifndef VCAP_ATTN_WAVES_PER_SIMD
+#define VCAP_ATTN_WAVES_PER_SIMD 1
+#endif
+
 VCAP_DEV void glds16_attn(const void* g, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
@@ -298,7 +306,9 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
     for (int dt = 0; dt < 4; ++dt) {
       const int ch = 2 * dt + (p4 >> 1);
       const u32x2 lo = tr_read(Vs + r0 * 128 + ((ch ^ (r0 & 7)) << 4) + 8 * (p4 & 1));
-      const u32x2 hi = tr_read(Vs + r1 * 128 + ((ch ^ (r1 & 7)) << 4) + 8 * (p4 & 1));
+      // keys 16 KE .. 16 KT - 1 are all padding (P = 0): not staged, a zero operand instead
+      const u32x2 hi = (KE < KT && c == KT / 2 - 1) ? (u32x2){0u, 0u}
+                                                    : tr_read(Vs + r1 * 128 + ((ch ^ (r1 & 7)) << 4) + 8 * (p4 & 1));
       o[dt] = mfma_frag((u32x4){lo.x, lo.y, hi.x, hi.y}, pf, o[dt], (bf16_t*)nullptr);
     }
 #if !defined(VCAP_ATTN_VALU_SUM) && !defined(VCAP_ATTN_PACKED_SOFTMAX)
@@ -392,16 +402,17 @@ VCAP_DEV void attn_commit(const AttnOut& r, void* out, int D, int h, uint8_t* os
 // MXO: write the output as MXFP8 (e4m3 + E8M0 per 32 of the head's 64 dims) for an MXFP8 attn-proj
 // GEMM; oscale in the vcap_common.h layout over `groups` 256-row groups.
 template <int KT, int KE, int WAVES, bool MXO>
-__global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(const bf16_t* __restrict__ qkv,
+__global__ __launch_bounds__(WAVES * 64, KT == 14 ? VCAP_ATTN_WAVES_PER_SIMD : 1) void vcap_vit_attention_bf16_kernel(const bf16_t* __restrict__ qkv,
                                                                              void* __restrict__ out, int N, int H,
                                                                              uint8_t* __restrict__ oscale,
                                                                              int groups, int cls_only) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NP = KT * 16;
+  constexpr int NS = KE * 16;  // staged key rows (the all-padding last tile is never read)
   constexpr int QT_MAX = (KT + WAVES - 1) / WAVES;  // query tiles per wave (N <= NP)
   static_assert(KT % 2 == 0, "PV consumes 32-key chunks");
   char* Ks = smem;
-  char* Vs = smem + NP * 128;
+  char* Vs = smem + NS * 128;
 
   const int bh = blockIdx.x;
   const int bt = bh / H, h = bh - bt * H;
@@ -414,7 +425,7 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
 
   // ---- K, V -> LDS by DMA (rows past N re-read row N-1: finite, masked out of the softmax)
 #ifndef VCAP_DIAG_ATTN_NOLOAD
-  for (int blk = wave; blk < NP / 8; blk += WAVES) {
+  for (int blk = wave; blk < NS / 8; blk += WAVES) {
     const int r = blk * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (r & 7);
     const bf16_t* src = base + (long)min(r, N - 1) * ld + c * 8;
@@ -422,6 +433,7 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
     glds16_attn(src + 2 * D, Vs + blk * 1024);
   }
 #endif
+  (void)NP;
   // ---- this wave's Q fragments
   const int qtiles = cls_only ? 1 : (N + 15) / 16;
   u32x4 qf[QT_MAX][2];
@@ -566,7 +578,7 @@ static bool attn_pipe_enabled() {
 template <int KT, int KE, int WAVES, bool MXO>
 static hipError_t launch_attn_bf16(const void* qkv, void* out, int BT, int N, int H, uint8_t* oscale, int cls_only,
                                    hipStream_t s) {
-  const size_t lds = (size_t)KT * 16 * 128 * 2;
+  const size_t lds = (size_t)KE * 16 * 128 * 2;  // 53 KiB at KE = 13: three workgroups per CU
   static bool configured = false;
   if (!configured) {
     hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_bf16_kernel<KT, KE, WAVES, MXO>,

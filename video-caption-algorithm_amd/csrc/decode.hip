@@ -18,6 +18,15 @@
 // so every weight load is one fully coalesced 1 KiB wave instruction and a wave's whole K range
 // of a tile is one contiguous run (rows >= N are zero).
 #include "vcap_common.h"
+// Weight fragments: buffer loads (SGPR base = the kernel argument, one VGPR byte offset) with the
+// nontemporal policy.  nt keeps the decode's 247 MB per token step from evicting the concurrently
+// running encode's operand tiles (plain loads: encode stage +2 %, bench -2 %); the buffer form
+// instead of flat global loads cut the decode step 269.7 -> 263.5 us alone
+// (profiles/r02_decode_experiments.txt).  Policy bits on gfx950: 1 = sc0, 2 = nt, 16 = sc1.
+__device__ __forceinline__ u32x4 vcap_dec_wload(const void* base, const void* p) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7FFFFFFF, 0x00020000);
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)((const char*)p - (const char*)base), 0, 2));
+}
 #include "vcap_kernels.h"
 
 #include <algorithm>
@@ -240,7 +249,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   for (int j = 0; j < NTB; ++j) {
     const u32x4* wp = packed_frag(a.w, min(n0 / 16 + j, ntiles - 1), nslab, g0, lane);
 #pragma unroll
-    for (int s = 0; s < NSL; ++s) wf[s][j] = __builtin_nontemporal_load(wp + s * 64);
+    for (int s = 0; s < NSL; ++s) wf[s][j] = vcap_dec_wload(a.w, wp + s * 64);
   }
 
   // ---- 3) epilogue inputs
@@ -441,7 +450,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
       }
 #pragma unroll
       for (int j = 0; j < NTB; ++j)
-        wf[u][j] = __builtin_nontemporal_load(
+        wf[u][j] = vcap_dec_wload(a.w,
             packed_frag(a.w, min(n0 / 16 + j, ntiles - 1), nslab, g0 + sl, lane));
     }
   };
@@ -807,6 +816,8 @@ static bool try_gemv(int nsl, const RowsGemmArgs& a, hipStream_t s, hipError_t& 
 
 template <typename T, int MT, int NTB, int PRO, int EPI>
 static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
+  // the weight loads address the packed matrix with a 32-bit byte offset (vcap_dec_wload)
+  if ((long)(a.N + 63) * a.K * (long)sizeof(T) >= 0x7FFFFFFFL) return hipErrorInvalidValue;
   const int nsl = a.K / (16 * Frag<T>::kElems);
   hipError_t err = hipSuccess;
   if (try_gemv<T, MT, NTB, PRO, EPI, 6>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 8>(nsl, a, s, err) ||

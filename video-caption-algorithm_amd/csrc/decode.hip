@@ -22,10 +22,15 @@
 // nontemporal policy.  nt keeps the decode's 247 MB per token step from evicting the concurrently
 // running encode's operand tiles (plain loads: encode stage +2 %, bench -2 %); the buffer form
 // instead of flat global loads cut the decode step 269.7 -> 263.5 us alone
-// (profiles/r02_decode_experiments.txt).  Policy bits on gfx950: 1 = sc0, 2 = nt, 16 = sc1.
-__device__ __forceinline__ u32x4 vcap_dec_wload(const void* base, const void* p) {
+// (profiles/r02_decode_experiments.txt); the GEMV's activation / LayerNorm operands use the same
+// form with the default policy (263.4 -> 261.0 us).  Policy bits on gfx950: 1 = sc0, 2 = nt, 16 = sc1.
+template <int AUX = 0>
+__device__ __forceinline__ u32x4 vcap_buf_load16(const void* base, long off_bytes) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7FFFFFFF, 0x00020000);
-  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)((const char*)p - (const char*)base), 0, 2));
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off_bytes, 0, AUX));
+}
+__device__ __forceinline__ u32x4 vcap_dec_wload(const void* base, const void* p) {
+  return vcap_buf_load16<2>(base, (const char*)p - (const char*)base);
 }
 #include "vcap_kernels.h"
 
@@ -222,22 +227,21 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   if constexpr (PRO == PRO_DIRECT) {
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      const T* xr = (const T*)a.x + (long)min(m0 + i * 16 + fr, M - 1) * a.ldx + fg * E;
+      const long xo = (long)min(m0 + i * 16 + fr, M - 1) * a.ldx + fg * E;
 #pragma unroll
-      for (int s = 0; s < NSL; ++s) af[i][s] = *reinterpret_cast<const u32x4*>(xr + (g0 + s) * KS);
+      for (int s = 0; s < NSL; ++s) af[i][s] = vcap_buf_load16(a.x, (xo + (g0 + s) * KS) * (long)sizeof(T));
     }
   } else {
-    const float* X = (const float*)a.x;
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
-      const float* xr = X + (long)min(m0 + wave + 4 * r, M - 1) * a.ldx + lane * 4;
+      const long xo = (long)min(m0 + wave + 4 * r, M - 1) * a.ldx + lane * 4;
 #pragma unroll
-      for (int c = 0; c < KC; ++c) xv[r][c] = *reinterpret_cast<const f32x4*>(xr + c * 256);
+      for (int c = 0; c < KC; ++c) xv[r][c] = __builtin_bit_cast(f32x4, vcap_buf_load16(a.x, (xo + c * 256) * 4L));
     }
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
-      gv[c] = *reinterpret_cast<const f32x4*>(a.ln_g + c * 256 + lane * 4);
-      bv[c] = *reinterpret_cast<const f32x4*>(a.ln_b + c * 256 + lane * 4);
+      gv[c] = __builtin_bit_cast(f32x4, vcap_buf_load16(a.ln_g, (c * 256 + lane * 4) * 4L));
+      bv[c] = __builtin_bit_cast(f32x4, vcap_buf_load16(a.ln_b, (c * 256 + lane * 4) * 4L));
     }
   }
 

@@ -197,16 +197,60 @@ def decode_step_alone(dec, prefix, ids_cfg, ga):
     return (res[ids_cfg.max_new_tokens] - res[lo]) / (ids_cfg.max_new_tokens - lo), res[lo]
 
 
-def token_agreement(got, ref):
-    """(mean fraction of leading tokens equal per caption, position-wise agreement)."""
-    lead = []
-    for a, b in zip(got, ref):
-        n = 0
-        while n < len(b) and a[n] == b[n]:
-            n += 1
-        lead.append(n / len(b))
-    return sum(lead) / len(lead), sum(int(x == y) for a, b in zip(got, ref) for x, y in zip(a, b)) / (
-        len(ref) * len(ref[0]))
+def describe(xs):
+    """mean / std / p50 / p99 / min / max (the reference's stage statistics plus p50)."""
+    import numpy as np
+    a = np.asarray(xs, dtype=np.float64)
+    return {"mean": float(a.mean()), "std": float(a.std()), "p50": float(np.median(a)),
+            "p99": float(np.percentile(a, 99)), "min": float(a.min()), "max": float(a.max()), "n": int(a.size)}
+
+
+def launch_summary(launches, rows_main, flops_of, bytes_of=None):
+    """Per-launch probe records [(ms, rows)] -> the population of full-group launches (rows_main
+    rows) priced with its own FLOPs, plus every other population (a flushed partial group)."""
+    from vcap import probe
+    pops = probe.by_rows(launches)
+    main = pops.get(rows_main) or max(pops.values(), key=len)
+    r_main = rows_main if rows_main in pops else max(pops, key=lambda r: len(pops[r]))
+    out = {"launches": len(main), "avg_launch_ms": sum(main) / len(main), "flops_per_launch": flops_of(r_main),
+           "other_populations": {str(r): {"launches": len(v), "avg_launch_ms": sum(v) / len(v)}
+                                 for r, v in pops.items() if r != r_main}}
+    if bytes_of is not None:
+        out["bytes_per_launch"] = bytes_of(r_main)
+    return out
+
+
+def parity_report(sd, va, ga, video, pre, enc, dec, cfg, last, dev):
+    """The benchmarked precision against the fp32 parity mode on the benchmark's own frames.
+    Greedy: every divergent caption is explained by the fp32 margin at its first divergent step
+    against the tested precision's teacher-forced logit error (vcap.fidelity.greedy_divergence).
+    Beam search: the fp32 score of the tested search's best hypothesis against the fp32 search's
+    (vcap.fidelity.beam_divergence)."""
+    import torch
+    from vcap import fidelity
+    from vcap.model import HipGPT2Decoder, HipViTEncoder
+    enc32 = HipViTEncoder(sd, va, "fp32", dev)
+    dec32 = HipGPT2Decoder(sd, ga, "fp32", dev)
+    _, pre32 = enc32.encode(video, pre)
+    prompt = [ga.bos_token_id]
+    L, B = cfg.max_new_tokens, video.shape[0]
+    against = "fp32 parity mode on the same frames (token-identical to the reference goldens)"
+    if cfg.num_beams > 1:
+        ids32 = dec32.generate_ids(pre32, prompt, cfg).cpu()
+        rep = fidelity.beam_divergence(dec32, pre32, prompt, last.tolist(), ids32.tolist(), cfg)
+        rep.update({"against": against, "batch": "last timed batch"})
+        return rep
+    logits32 = torch.empty(L, B, ga.vocab, dtype=torch.float32, device=dev)
+    ids32 = dec32.generate_ids(pre32, prompt, cfg, out=torch.empty(B, L, dtype=torch.int32, device=dev),
+                               logits_out=logits32)
+    _, pre_t = enc.encode(video, pre)
+    tf = fidelity.teacher_forced_logits(dec, pre_t, prompt, ids32, L)
+    rep = fidelity.greedy_divergence(last.numpy(), ids32.cpu().numpy(), logits32, tf, cfg)
+    rep.update({"against": against, "batch": "last timed batch",
+                "evidence": "tested-precision encoder + decoder teacher-forced along the fp32 tokens; "
+                            "fp32_margin = fp32 processed score of its token minus that of the tested "
+                            "path's token at the first divergent step"})
+    return rep
 
 
 def workload_tag(args, world):
@@ -223,7 +267,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from vcap import configs, prng, weights
+    from vcap import configs, prng, probe, weights
     from vcap import _native as N
     from vcap.model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder
     from vcap.pipeline import CaptionPipeline
@@ -297,10 +341,11 @@ def main():
         gather_ids(ids_all, world)  # communicator set-up outside the timed region
         torch.cuda.synchronize(dev)
         dist.barrier()
-    lib = N.lib()
-    fc1_launches = va.depth * args.steps
-    N.check(lib.vcap_probe_enable(b"vit.fc1", fc1_launches), "probe")
-    N.check(lib.vcap_probe_enable(b"vit.attention", fc1_launches), "probe")
+    # live per-launch timing of the dominant encode kernels inside the timed region only: enabled
+    # here, read (and disabled) right after it, before any other leg launches an encode
+    probe_cap = va.depth * (args.steps + 2)
+    for site in ("vit.fc1", "vit.attention"):
+        probe.enable(site, probe_cap)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     mids = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -318,6 +363,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    probes = {site: probe.read(site, probe_cap) for site in ("vit.fc1", "vit.attention")}
+    E_enc = 1 if args.serial else args.enc_group
+    enc_launches = -(-args.steps // E_enc)          # encodes issued in the timed region (a trailing
+    expected = enc_launches * (va.depth - 1)        # partial group is flushed inside it)
+    for site, launches in probes.items():
+        if len(launches) != expected:
+            raise RuntimeError(f"probe {site}: {len(launches)} launches in the timed region, expected {expected}")
 
     # SURVEY 8(d) latency: a host-pinned [B,T,3,H,W] fp32 tensor -> H2D -> encode -> decode ->
     # token ids on the host, one batch at a time (outside the timed throughput region)
@@ -342,20 +394,12 @@ def main():
     # caption lengths of the last timed batch (new tokens up to and including EOS)
     last = pipe.result(pipe.last_slot).cpu()
     # parity of what was timed (outside the timed region): the last batch's ids against the fp32
-    # parity mode (token-exact against the reference: tests/test_gpu_parity.py) on the same frames
+    # parity mode (token-exact against the reference: tests/test_gpu_parity.py) on the same frames,
+    # with the near-tie evidence for every divergent caption (vcap/fidelity.py)
     parity = None
     dec_alone = None
     if args.precision != "fp32" and args.parity:
-        enc32 = HipViTEncoder(sd, va, "fp32", dev)
-        dec32 = HipGPT2Decoder(sd, ga, "fp32", dev)
-        _, pre32 = enc32.encode(video, pre)
-        ids32 = dec32.generate_ids(pre32, [ga.bos_token_id], cfg).cpu()
-        lead, pos = token_agreement(last.tolist(), ids32.tolist())
-        parity = {"against": "fp32 parity mode on the same frames (token-identical to the reference goldens)",
-                  "batch": "last timed batch", "leading_token_agreement": lead, "position_agreement": pos,
-                  "captions_identical": int(sum(a == b for a, b in zip(last.tolist(), ids32.tolist()))),
-                  "captions": int(last.shape[0])}
-        del enc32, dec32, pre32
+        parity = parity_report(sd, va, ga, video, pre, enc, dec, cfg, last, dev)
         torch.cuda.empty_cache()
     if args.decode_alone:
         with torch.cuda.stream(torch.cuda.Stream(dev)):
@@ -378,22 +422,25 @@ def main():
     lat = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     vit_ms = [s.elapsed_time(m) for s, m in zip(starts, mids)]
     dec_ms = [m.elapsed_time(e) for m, e in zip(mids, ends)]
-    fc1_total, fc1_n = N.C.c_float(), N.C.c_int()
-    N.check(lib.vcap_probe_read(b"vit.fc1", N.C.byref(fc1_total), N.C.byref(fc1_n)), "probe read")
-    at_total, at_n = N.C.c_float(), N.C.c_int()
-    N.check(lib.vcap_probe_read(b"vit.attention", N.C.byref(at_total), N.C.byref(at_n)), "probe read")
 
     if rank == 0:
         E = 1 if args.serial else args.enc_group   # batches per encode launch
-        M = E * B * T * va.tokens                    # ViT rows per GEMM launch
-        fc1_flops = 2.0 * M * va.mlp * va.dim
-        fc1_avg_s = fc1_total.value / max(fc1_n.value, 1) / 1e3
+        M = E * B * T * va.tokens                    # ViT rows per GEMM launch (full encode group)
         peak = {"bf16": PEAK_BF16_TFLOPS, "fp8": PEAK_FP8_TFLOPS}.get(args.precision, PEAK_F32_TFLOPS)
-        achieved = fc1_flops / fc1_avg_s / 1e12
-        attn_flops = 4.0 * E * B * T * va.heads * va.tokens * va.tokens * 64
-        attn_avg_s = at_total.value / max(at_n.value, 1) / 1e3
         ab = 2 if args.precision in ("bf16", "fp8") else 4
-        attn_bytes = float(M * 3 * va.dim * ab + M * va.dim * (1 if args.precision == "fp8" else ab))
+
+        def fc1_flops(rows):
+            return 2.0 * rows * va.mlp * va.dim
+
+        def attn_flops(rows):
+            return 4.0 * (rows // va.tokens) * va.heads * va.tokens * va.tokens * 64
+
+        def attn_bytes(rows):
+            return float(rows * 3 * va.dim * ab + rows * va.dim * (1 if args.precision == "fp8" else ab))
+
+        fc1 = launch_summary(probes["vit.fc1"], M, fc1_flops)
+        att = launch_summary(probes["vit.attention"], M, attn_flops, attn_bytes)
+        achieved = fc1["flops_per_launch"] / (fc1["avg_launch_ms"] / 1e3) / 1e12
         vit_exec = B * T * va.flops_per_frame(cls_tail=True)
         dec_bytes = float(args.max_new * ga.weight_elems_per_step() * (4 if args.precision == "fp32" else 2))
         t_roof = vit_exec / (peak * 1e12) + dec_bytes / (PEAK_HBM_GBS * 1e9)
@@ -431,6 +478,10 @@ def main():
                                        "decode_steps_run": args.max_new},
             "stage_ms_p50": {"vit_encode_prefix": statistics.median(vit_ms),
                              "prefix_ready_to_ids": statistics.median(dec_ms)},
+            # the reference's per-stage statistics (core/scripts/benchmark_baseline.py:114-139) over the
+            # timed steps: batch latency (encode start -> ids), encode (+ prefix), prefix-ready -> ids
+            "latency_ms_stats": {"end_to_end": describe(lat), "vit_encode_prefix": describe(vit_ms),
+                                 "prefix_ready_to_ids": describe(dec_ms)},
             "roofline": {"bound": "mfma",
                          "kernel": {"bf16": "vit.fc1 vcap_gemm256_kernel<bf16,bf16,1>",
                                     "fp8": "vit.fc1 vcap_gemm256_kernel<mxfp8,mxfp8,4>"}.get(
@@ -438,14 +489,19 @@ def main():
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": fc1_traffic(M, va.mlp, va.dim) if args.precision == "bf16" else None,
                          "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                         "flops_per_launch": fc1_flops, "avg_launch_ms": fc1_avg_s * 1e3,
-                         "launches": fc1_n.value},
-            "attention": {"kernel": "vit.attention", "bound": "hbm", "avg_launch_ms": attn_avg_s * 1e3,
-                          "achieved_tflops": attn_flops / attn_avg_s / 1e12,
-                          "frac_of_mfma_peak": attn_flops / attn_avg_s / 1e12 / peak,
-                          "bytes_per_launch": attn_bytes,
-                          "achieved_gbs": attn_bytes / attn_avg_s / 1e9,
-                          "frac_of_hbm_peak": attn_bytes / attn_avg_s / 1e9 / PEAK_HBM_GBS},
+                         "flops_per_launch": fc1["flops_per_launch"], "avg_launch_ms": fc1["avg_launch_ms"],
+                         "launch_rows": M, "launches": fc1["launches"],
+                         "timing": "HIP events around each fc1 launch on its stream inside the timed region "
+                                   "(vcap_probe_*), read right after it; priced per launch population",
+                         "other_populations": fc1["other_populations"]},
+            "attention": {"kernel": "vit.attention", "bound": "hbm", "avg_launch_ms": att["avg_launch_ms"],
+                          "launch_rows": M, "launches": att["launches"],
+                          "achieved_tflops": att["flops_per_launch"] / (att["avg_launch_ms"] / 1e3) / 1e12,
+                          "frac_of_mfma_peak": att["flops_per_launch"] / (att["avg_launch_ms"] / 1e3) / 1e12 / peak,
+                          "bytes_per_launch": att["bytes_per_launch"],
+                          "achieved_gbs": att["bytes_per_launch"] / (att["avg_launch_ms"] / 1e3) / 1e9,
+                          "frac_of_hbm_peak": att["bytes_per_launch"] / (att["avg_launch_ms"] / 1e3) / 1e9 / PEAK_HBM_GBS,
+                          "other_populations": att["other_populations"]},
             # whole-path roofline: executed ViT FLOPs at the MFMA peak + the decode's
             # weight bytes (every token step streams all projection weights + the tied lm_head) at
             # the HBM peak, against the measured time per batch
@@ -461,6 +517,7 @@ def main():
         if host_lat:
             hp50 = statistics.median(host_lat)
             out["host_e2e"] = {"p50_ms": hp50 * 1e3, "captions_per_s": world * B / hp50, "iters": len(host_lat),
+                               "stats_ms": describe([x * 1e3 for x in host_lat]),
                                "h2d_bytes": int(video.numel() * video.element_size()),
                                "what": "pinned host fp32 frames -> H2D -> encode -> decode -> ids on host, "
                                        "one batch at a time (no overlap; rank 0's clock)"}

@@ -107,10 +107,13 @@ class InferenceEngine:
                                  device=self.device)
 
     def max_batch_videos(self) -> int:
-        """Videos one infer_videos call can decode: every candidate's prefill takes
-        B * (prefix_len + prompt_len) decoder rows and a beam candidate B * num_beams rows, both
-        within vcap_gpt2_max_rows()."""
+        """Videos one device call decodes at once: a greedy / sampling candidate's prefill takes
+        B * (prefix_len + prompt_len) decoder rows, within vcap_gpt2_max_rows(); a beam candidate
+        is chunked by the decoder itself (vcap.search.beam_search_any), so this only sizes the
+        coalesced batch to what one device beam chunk takes - at most 8 sequences and
+        B * num_beams * (prefix_len + prompt_len) rows - to keep every chunk full."""
         from vcap import _native as N
+        from vcap.search import BEAM_DEVICE_MAX_B
         c, tok = self.config, self.model.decoder.tokenizer
         rows = limit = int(N.lib().vcap_gpt2_max_rows())
         for prompt, preset in ((c.prompt1, c.preset1), (c.prompt2, c.preset2), (c.prompt3, c.preset3)):
@@ -119,7 +122,9 @@ class InferenceEngine:
             except ValueError:
                 s0 = c.prefix_len + 1   # an untokenizable prompt fails per request anyway
             beams = max(1, preset_to_kwargs(preset).get("num_beams", 1))
-            rows = min(rows, limit // s0, limit // beams, 8 if beams > 1 else limit)  # device beam: B <= 8
+            rows = min(rows, limit // s0)
+            if beams > 1:
+                rows = min(rows, BEAM_DEVICE_MAX_B, limit // (beams * s0))
         return max(1, rows)
 
     @torch.no_grad()

@@ -14,7 +14,8 @@ semantics.
 A request must fail alone, as it would in the reference's one-request-per-call service: videos
 are loaded per request (a bad frames_dir fails only its own request), grouped by shape (frame
 count and size: torch.cat of different clips would fail the whole call), cut into chunks the
-decoder takes in one call (engine.max_batch_videos(): B * (prefix + prompt) <= 128 decode rows),
+decoder takes in one call (engine.max_batch_videos(): B * (prefix + prompt) <= vcap_gpt2_max_rows()
+= 512 decode rows, and one full device beam chunk: <= 8 sequences, B * beams * (prefix + prompt) <= 512),
 and a chunk whose engine call fails is retried one request at a time so only the offending
 request gets the error.
 """

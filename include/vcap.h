@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 6
+#define VCAP_ABI_VERSION 8
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -196,6 +196,25 @@ size_t vcap_gpt2_workspace_bytes(const vcap_gpt2_desc* d, int B, int S0, int max
 int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* prompt_ids,
                        int prompt_len, int B, int* out_ids, float* logits_out, void* workspace, size_t ws_bytes,
                        void* stream);
+/* ---- sampling presets (core/inference.py:12-15 natural / safe_sample; HF _sample as
+ *      text_decoder.py:131-144 reaches it with do_sample = num_beams == 1 and temperature != 1):
+ *      the greedy decode's processors, then TemperatureLogitsWarper -> TopKLogitsWarper(top_k) ->
+ *      TopPLogitsWarper(top_p) -> one multinomial draw per row and step from a counter-based
+ *      Philox4x32-10 stream keyed on `seed` (csrc/sample.hip).  The same hipGraph serves every seed.
+ *      warped_out (optional, [max_new][B][vocab] f32): the warped scores each draw used (-inf where
+ *      removed), i.e. HF's output_scores; force_ids (optional, [B][max_new]): emit these tokens
+ *      instead of drawing (tests replay a recorded history).  Parity with the reference is
+ *      distributional: the RNG streams differ. ---- */
+typedef struct vcap_sample_params {
+  float temperature;  /* > 0 */
+  int top_k;          /* HF generation-config default 50; 1..128 */
+  double top_p;       /* (0, 1] */
+  uint64_t seed;
+} vcap_sample_params;
+int vcap_gpt2_sample(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const vcap_sample_params* sp,
+                     const float* prefix, const int* prompt_ids, int prompt_len, int B, int* out_ids,
+                     float* logits_out, float* warped_out, const int* force_ids, void* workspace, size_t ws_bytes,
+                     void* stream);
 void vcap_graph_cache_clear(void);
 /* number of instantiated decode graphs held by the cache (bounded LRU, VCAP_GRAPH_CACHE_MAX) */
 int vcap_graph_cache_size(void);
@@ -261,6 +280,9 @@ int vcap_gpt2_forward_embeds(const vcap_gpt2_desc* d, const float* embeds, int r
  *      the caller's stream, without synchronising; vcap_probe_read waits for them. ---- */
 int vcap_probe_enable(const char* site, int max_launches);
 int vcap_probe_read(const char* site, float* total_ms, int* launches);
+/* Per-launch form: ms[i] / rows[i] (the launch's GEMM or attention rows) for each of the *launches
+ * (<= cap) recorded launches; like vcap_probe_read it disables the site. */
+int vcap_probe_read_launches(const char* site, float* ms, int* rows, int cap, int* launches);
 
 #ifdef __cplusplus
 }

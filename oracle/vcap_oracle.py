@@ -325,6 +325,35 @@ def generate_beam(sd, arch, inputs_embeds: Tensor, *, num_beams: int, max_new_to
     return seqs[:, 0, :n].tolist()
 
 
+def hypothesis_scores(sd, arch, inputs_embeds: Tensor, seqs: Sequence[Sequence[int]], *, min_new_tokens: int = 8,
+                      repetition_penalty: float = 1.1, no_repeat_ngram_size: int = 3, length_penalty: float = 1.0,
+                      eos_token_id: Optional[int] = None) -> List[float]:
+    """The score HF _beam_search gives a finished hypothesis (transformers 5.15.0
+    generation/utils.py:3182 `_update_finished_beams`: the running sum of processed log-probs /
+    generated length ** length_penalty; generate_beam above accumulates exactly that), computed
+    for given token sequences teacher-forced from inputs_embeds (row i continues row i)."""
+    eos = arch.eos_token_id if eos_token_id is None else eos_token_id
+    seqs = [list(map(int, r)) for r in seqs]
+    lens = [r.index(eos) + 1 if eos in r else len(r) for r in seqs]
+    L = max(lens)
+    tok = torch.full((len(seqs), L), eos, dtype=torch.long)
+    for i, r in enumerate(seqs):
+        tok[i, :lens[i]] = torch.tensor(r[:lens[i]])
+    cache = KVCache(arch.n_layer)
+    wte = _t(sd, "decoder.model.transformer.wte.weight")
+    x = inputs_embeds
+    total = torch.zeros(len(seqs), dtype=torch.float64)
+    for s in range(L):
+        lp = torch.log_softmax(gpt2_forward(sd, arch, x, cache)[:, -1, :].float(), dim=-1)
+        lp = process_logits(lp, tok[:, :s], repetition_penalty=repetition_penalty,
+                            no_repeat_ngram_size=no_repeat_ngram_size, min_new_tokens=min_new_tokens,
+                            eos_token_id=eos)
+        live = torch.tensor([s < n for n in lens])
+        total += torch.where(live, lp.gather(1, tok[:, s:s + 1])[:, 0].double(), torch.zeros_like(total))
+        x = wte[tok[:, s]].unsqueeze(1)
+    return (total / torch.tensor(lens, dtype=torch.float64) ** length_penalty).tolist()
+
+
 def caption_ids(sd, vit_arch, gpt_arch, video: Tensor, prompt_ids: Sequence[int], *, ln_scale: float = 0.6,
                 in_weight: float = 0.4, prefix_len: int = 4, mode: str = "hf_greedy", **gen_kw):
     """Engine path A1 (core/engine.py:39-64) up to token ids (before detokenize/clean_text)."""

@@ -197,3 +197,15 @@ def test_oracle_beam_matches_reference_b16_b2(nb, mx):
     with torch.no_grad():
         rows = O.generate_beam(sd, ga, x, num_beams=nb, max_new_tokens=mx)
     assert np.array_equal(np.array(rows, dtype=np.int32), g[f"beam{nb}_ids"])
+
+
+@pytest.mark.parametrize("name,nb", [("b16_b2", 3), ("b16_b2", 4), ("l14_medium", 4)])
+def test_oracle_hypothesis_scores_match_reference_beam_scores(name, nb):
+    """Rescoring the reference's returned beam hypotheses (HF `sequences_scores`, recorded by
+    make_goldens.py) with the processed-log-prob / length formula that vcap.fidelity uses to price
+    a reduced-precision beam search reproduces the reference's scores."""
+    meta, g, va, ga, sd, frames = case(name)
+    x = torch.from_numpy(g["inputs_embeds"].copy())
+    with torch.no_grad():
+        got = O.hypothesis_scores(sd, ga, x, g[f"beam{nb}_ids"].tolist())
+    np.testing.assert_allclose(got, g[f"beam{nb}_scores"], rtol=0, atol=2e-5)

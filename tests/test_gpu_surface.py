@@ -83,22 +83,67 @@ def test_repeated_generate_once_reuses_one_graph(device):
 
 
 @pytest.mark.parametrize("preset", ["natural", "safe_sample"])
-def test_sampling_scores_match_hf_warpers(device, preset):
-    """The distribution `natural` / `safe_sample` draw from: HIP-side processors + Temperature +
-    TopP applied to the reference's raw logits with the reference's sampled history equal HF's
-    processed scores (same -inf mask, finite scores within 1e-5), every step."""
-    meta, g = golden("tiny")
+def test_device_sampling_warped_scores_match_hf_every_step(device, preset):
+    """The distribution `natural` / `safe_sample` draw from, computed by the device sampling path
+    (lm_head processor epilogue + csrc/sample.hip warpers inside the decode graph), replaying the
+    reference's own sampled history (force_ids): at every step the warped scores (warped_out) equal
+    HF's processed scores (same -inf mask, finite scores within 1e-4) and the raw logits equal the
+    reference's (tests/golden/tiny, make_goldens.py surface_case)."""
+    from vcap.model import GenConfig, HipGPT2Decoder
+    meta, g, va, ga, sd, frames = case("tiny")
     kw = meta[preset]
     logits = torch.from_numpy(g[f"{preset}_logits"]).to(device)    # [steps, B, V]
     scores = torch.from_numpy(g[f"{preset}_scores"]).to(device)
-    ids = torch.from_numpy(g[f"{preset}_ids"].astype(np.int64)).to(device)
-    for s in range(logits.shape[0]):
-        got = search.sampling_scores(logits[s], ids[:, :s], temperature=kw["temperature"], top_p=kw["top_p"],
-                                     rep=kw["repetition_penalty"], ngram=kw["no_repeat_ngram_size"],
-                                     min_new=kw["min_new_tokens"], eos=1023)
+    ids = g[f"{preset}_ids"].astype(np.int64)
+    steps, B = logits.shape[0], logits.shape[1]
+    L = kw["max_new_tokens"]
+    force = np.full((B, L), ga.eos_token_id, np.int64)
+    force[:, :ids.shape[1]] = ids
+    dec = HipGPT2Decoder(sd, ga, "fp32", device)
+    cfg = GenConfig(L, kw["min_new_tokens"], kw["no_repeat_ngram_size"], kw["repetition_penalty"], ga.eos_token_id,
+                    ga.eos_token_id, True, temperature=kw["temperature"], top_p=kw["top_p"], seed=5)
+    prefix = torch.from_numpy(g["inputs_embeds"][:, :4].copy()).to(device)
+    warped = torch.empty(L, B, ga.vocab, device=device)
+    raw = torch.empty(L, B, ga.vocab, device=device)
+    out = dec.generate_ids(prefix, [ga.bos_token_id], cfg, logits_out=raw, warped_out=warped,
+                           force_ids=torch.from_numpy(force))
+    assert np.array_equal(out.cpu().numpy()[:, :ids.shape[1]], ids)
+    for s in range(steps):
+        torch.testing.assert_close(raw[s], logits[s], rtol=0, atol=1e-4)
         fin = torch.isfinite(scores[s])
-        assert torch.equal(torch.isfinite(got), fin), s
-        torch.testing.assert_close(got[fin], scores[s][fin], rtol=1e-5, atol=1e-5)
+        assert torch.equal(torch.isfinite(warped[s]), fin), s
+        torch.testing.assert_close(warped[s][fin], scores[s][fin], rtol=1e-5, atol=1e-4)
+
+
+def test_device_sampling_draws_follow_the_warped_distribution(device):
+    """3200 first-token draws (100 rows x 32 seeds) of one prefix: every draw lies in the warped
+    support, and the draw frequencies match softmax(warped scores) (chi-square, pooled bins)."""
+    from scipy import stats
+    from vcap.model import GenConfig, HipGPT2Decoder
+    meta, g, va, ga, sd, frames = case("tiny")
+    dec = HipGPT2Decoder(sd, ga, "fp32", device)
+    rows = 100
+    prefix = torch.from_numpy(np.repeat(g["inputs_embeds"][:1, :4], rows, axis=0).copy()).to(device)
+    counts = np.zeros(ga.vocab)
+    probs = None
+    for seed in range(32):
+        cfg = GenConfig(1, 0, 3, 1.05, ga.eos_token_id, ga.eos_token_id, True, temperature=0.9, top_p=0.9, seed=seed)
+        warped = torch.empty(1, rows, ga.vocab, device=device)
+        ids = dec.generate_ids(prefix, [ga.bos_token_id], cfg, warped_out=warped).cpu().numpy()[:, 0]
+        p = torch.softmax(warped[0, 0].double(), -1).cpu().numpy()
+        assert probs is None or np.allclose(p, probs)
+        probs = p
+        assert np.all(p[ids] > 0), "a draw outside the warped support"
+        np.add.at(counts, ids, 1)
+    n = counts.sum()
+    order = np.argsort(-probs)
+    big = [i for i in order if probs[i] * n >= 5]
+    f_obs = np.append(counts[big], n - counts[big].sum())
+    f_exp = np.append(probs[big] * n, n - probs[big].sum() * n)
+    keep = f_exp > 0
+    p_value = stats.chisquare(f_obs[keep], f_exp[keep]).pvalue
+    print(f"chi-square over {keep.sum()} bins: p = {p_value:.3g}")
+    assert p_value > 1e-4
 
 
 def test_checkpoint_roundtrip(device, tmp_path):

@@ -115,6 +115,7 @@ VCAP_DEV void rows_epilogue(const RowsGemmArgs& a, int m0, const float (*red)[MT
           if (s_rep[ml][j * 16 + col]) sv = sv < 0.f ? sv * a.rep_penalty : sv / a.rep_penalty;
           if (s_ban[ml][j * 16 + col]) sv = -INFINITY;
           if (n == a.eos && a.gen_len < a.min_new) sv = -INFINITY;
+          if (a.proc_out) a.proc_out[(long)m * N + n] = sv;
         }
         lg[ml][j * 16 + col] = sv;
       }

@@ -224,7 +224,10 @@ static hipError_t launch_gemm_epi(const void* A, long lda, const void* W, long l
   // only: the fp32 parity mode keeps one summation chain).  The split count depends on K alone
   // (the largest divisor c <= 8 of the K-tile count leaving >= 3 K-tiles per workgroup), never on
   // M or the stream's CU mask, so a row sums the same way whichever batch it is encoded in and a
-  // CU-masked pipelined encode sums exactly like a serial one.
+  // CU-masked pipelined encode sums exactly like a serial one.  (No CU-count gate: a large encode
+  // batch takes more rounds of split workgroups instead of switching the summation order.  The
+  // encoder's partials workspace holds 16 splits of its B*T CLS rows, so the size check below
+  // only refuses a caller-supplied workspace that is too small.)
   int splits = 1;
   if constexpr (sizeof(TIn) == 2 && sizeof(TOut) == 4) {
     const bool in_place = epi.bias != nullptr && epi.res == (const float*)C && epi.ldr == ldc &&
@@ -237,7 +240,7 @@ static hipError_t launch_gemm_epi(const void* A, long lda, const void* W, long l
         c = d;
         break;
       }
-    if (in_place && c > 1 && tiles * c <= vcap_device_cus() && (size_t)c * M * N * sizeof(float) <= epi.splitk_bytes)
+    if (in_place && c > 1 && (size_t)c * M * N * sizeof(float) <= epi.splitk_bytes)
       splits = c;
   }
   hipLaunchKernelGGL((vcap_gemm_kernel<TIn, TOut, EPI>), dim3(tiles, splits), dim3(256), 0, s, (const TIn*)A, lda,

@@ -555,7 +555,7 @@ static hipError_t launch256(const void* A, long lda, const void* W, long ldw, vo
     const bool plain_rows = epi.G == 0;
     if (plain_rows && epi.res_mode == 0 && epi.act == 0)
       return launch256_epi<TIn, TOut, 0>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
-    if constexpr (sizeof(TOut) == sizeof(TIn)) {
+    if constexpr (sizeof(TOut) == sizeof(TIn) || sizeof(TOut) == 2) {   // (MXFP8 in -> bf16 GELU out too)
       if (plain_rows && epi.res_mode == 0 && epi.act == 1)
         return launch256_epi<TIn, TOut, 1>(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
     }

@@ -66,6 +66,7 @@ constexpr int kMaxDecodeRows = 512;
 // probed site on the caller's stream (no synchronisation; read back after the timed region).
 struct Probe {
   std::vector<hipEvent_t> start, stop;
+  std::vector<int> rows;   // work size of each launch (GEMM / attention rows), for per-launch pricing
   int used = 0;
   bool on = false;
 };
@@ -83,9 +84,10 @@ struct ProbeScope {
   Probe* p;
   hipStream_t s;
   int idx;
-  ProbeScope(const char* site, hipStream_t st) : p(probe_for(site)), s(st), idx(-1) {
+  ProbeScope(const char* site, hipStream_t st, int rows) : p(probe_for(site)), s(st), idx(-1) {
     if (p) {
       idx = p->used++;
+      p->rows[idx] = rows;
       (void)hipEventRecord(p->start[idx], s);
     }
   }
@@ -117,11 +119,14 @@ VitBufs carve_vit(Carver& c, const vcap_vit_desc* d, int B, int T) {
   const size_t es = esize(d->dtype), ea = esize(vit_adt(d->dtype));
   const size_t npatch = (size_t)B * T * (tokens - 1);
   VitBufs v;
+  // MXFP8 mode: any GEMM of a layer may stay bf16 (its weight scales NULL), so the LayerNorm and
+  // fc1 outputs are sized for bf16 elements
+  const size_t en = es > ea ? es : ea;
   v.x = (float*)c.take(M * d->dim * 4);
-  v.xn = c.take(M * d->dim * es);
+  v.xn = c.take(M * d->dim * en);
   v.qkv = c.take(M * 3 * d->dim * ea);
   v.attn = c.take(M * d->dim * ea);
-  size_t act = M * d->mlp * es;
+  size_t act = M * d->mlp * en;
   const size_t patches = npatch * d->kpad * ea;
   v.act = c.take(act > patches ? act : patches);
   v.xn_s = v.act_s = nullptr;
@@ -143,10 +148,9 @@ int check_vit(const vcap_vit_desc* d) {
   if (d->dim % ka || d->mlp % ka || d->kpad % vcap_gemm_k_align(vit_adt(d->dtype)) || d->kpad < 3 * d->patch * d->patch)
     return fail(VCAP_E_UNSUPPORTED, "vit dims must be multiples of the GEMM K step");
   if (d->dtype == VCAP_DT_MXFP8) {
+    // per GEMM: weight scales present = MXFP8 block GEMM, NULL = that GEMM's weights are bf16
     if (d->dim > 1024) return fail(VCAP_E_UNSUPPORTED, "MXFP8 LayerNorm holds rows of <= 1024 in registers");
-    for (int l = 0; l < d->depth; ++l)
-      if (!d->layers[l].qkv_ws || !d->layers[l].proj_ws || !d->layers[l].fc1_ws || !d->layers[l].fc2_ws)
-        return fail(VCAP_E_ARG, "MXFP8 vit layer without weight scales");
+    if (d->dim % 256 || d->mlp % 256) return fail(VCAP_E_UNSUPPORTED, "MXFP8 dims must be multiples of 256");
   }
   if (d->image % d->patch) return fail(VCAP_E_ARG, "image not divisible by patch");
   const int tokens = (d->image / d->patch) * (d->image / d->patch) + 1;
@@ -169,6 +173,8 @@ struct DecBufs {
   int* banned;
   int* nbanned;
   int* finished;
+  float* proc;        // [B][V] processed scores (sampling mode)
+  unsigned* seed;     // [2] Philox key of the sampling draws
 };
 
 int max_logit_blocks(int V, int B) { return vcap_logit_blocks(V, B); }
@@ -197,6 +203,8 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.banned = (int*)c.take((size_t)B * max_new * 4);
   b.nbanned = (int*)c.take((size_t)B * 4);
   b.finished = (int*)c.take((size_t)B * 4);
+  b.proc = (float*)c.take((size_t)B * d->vocab * 4);
+  b.seed = (unsigned*)c.take(8);
   return b;
 }
 
@@ -290,7 +298,7 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
 // ln_f on each sequence's last row (fused into the lm_head's A prologue) + tied lm_head with the
 // fused processors and argmax partials.
 int run_lm_head(const vcap_gpt2_desc* d, const DecBufs& w, int rows, int S_new, float* logits_raw, int hist_ld,
-                int gen_len, float rep, int min_new, int eos, int* nblk, hipStream_t s) {
+                int gen_len, float rep, int min_new, int eos, int* nblk, hipStream_t s, float* proc_out = nullptr) {
   const int E = d->n_embd;
   RowsGemmArgs g;
   memset(&g, 0, sizeof(g));
@@ -302,13 +310,17 @@ int run_lm_head(const vcap_gpt2_desc* d, const DecBufs& w, int rows, int S_new, 
   g.nblk = max_logit_blocks(d->vocab, rows);
   g.hist = w.hist; g.hist_ld = hist_ld; g.gen_len = gen_len; g.banned = w.banned; g.nbanned = w.nbanned;
   g.rep_penalty = rep; g.min_new = min_new; g.eos = eos;
+  g.proc_out = proc_out;
   VCAP_TRY(vcap_rows_gemm_dispatch(d->dtype, PRO_LN, EPI_LOGITS, g, nblk, s), "lm_head");
   return 0;
 }
 
+// sp != nullptr: sampling mode (HF _sample): the lm_head also stores the processed scores, the
+// sample kernel warps them and draws (or takes force_ids), and hands the token to the finalize kernel
 int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* ids, int nids,
                  int B, int* out_ids, float* logits_out, const DecBufs& w, int maxp, size_t page_elems,
-                 hipStream_t s) {
+                 hipStream_t s, const vcap_sample_params* sp = nullptr, float* warped_out = nullptr,
+                 const int* force_ids = nullptr) {
   const int E = d->n_embd, V = d->vocab;
   const int P = d->prefix_len, S0 = P + nids, max_new = gp->max_new_tokens;
   const int dt = d->dtype;
@@ -320,8 +332,15 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
     if (int rc = run_layers(d, w, maxp, page_elems, B * S_new, S_new, past, gp->max_blocks, s)) return rc;
     int nblk = 0;
     if (int rc = run_lm_head(d, w, B, S_new, logits_out ? logits_out + (size_t)step * B * V : nullptr, max_new, step,
-                             gp->repetition_penalty, gp->min_new_tokens, gp->eos_token_id, &nblk, s))
+                             gp->repetition_penalty, gp->min_new_tokens, gp->eos_token_id, &nblk, s,
+                             sp ? w.proc : nullptr))
       return rc;
+    if (sp) {
+      SampleArgs sa{w.proc, V, V, sp->temperature, sp->top_k, sp->top_p, w.seed, step, force_ids, max_new,
+                    warped_out ? warped_out + (size_t)step * B * V : nullptr, V, w.pval, w.pidx};
+      VCAP_TRY(vcap_sample_dispatch(sa, B, s), "sample");
+      nblk = 1;
+    }
     VCAP_TRY(vcap_decode_finalize_dispatch(dt, w.pval, w.pidx, nblk, B, step, w.finished, w.hist, max_new, w.banned,
                                            w.nbanned, gp->no_repeat_ngram_size, gp->eos_token_id, gp->pad_token_id,
                                            out_ids, max_new, d->wte, d->wpe, w.h, E,
@@ -349,7 +368,9 @@ std::unordered_map<int, hipStream_t> g_capture_streams;
 size_t graph_cache_cap() {
   static size_t cap = [] {
     const char* e = std::getenv("VCAP_GRAPH_CACHE_MAX");
-    long v = e ? std::strtol(e, nullptr, 10) : 8;
+    // serving sees one greedy + one beam graph per (batch size, prompt, workspace): 64 entries keep a
+    // service whose coalesced batch sizes vary over 1..8 from re-capturing on every call
+    long v = e ? std::strtol(e, nullptr, 10) : 64;
     return (size_t)(v < 1 ? 1 : v);
   }();
   return cap;
@@ -365,16 +386,32 @@ void graph_entry_destroy(GraphEntry& ge) {
   ge.done = nullptr;
 }
 
-// caller holds g_graph_mu
-void graph_cache_evict_to(size_t n) {
+// caller holds g_graph_mu: unlink the least recently used entries down to n and hand them back, so
+// the caller destroys them (waiting for their last replay) after releasing the mutex - a wait under
+// the lock would stall every decode on other threads / streams
+std::vector<GraphEntry> graph_cache_evict_to(size_t n) {
+  std::vector<GraphEntry> out;
   while (g_graphs.size() > n && !g_graph_lru.empty()) {
     auto it = g_graphs.find(g_graph_lru.back());
     g_graph_lru.pop_back();
     if (it == g_graphs.end()) continue;
-    graph_entry_destroy(it->second);
+    out.push_back(it->second);
     g_graphs.erase(it);
   }
+  return out;
 }
+
+void graph_entries_destroy(std::vector<GraphEntry>& v) {
+  for (auto& ge : v) graph_entry_destroy(ge);
+  v.clear();
+}
+
+// evicted entries, destroyed when this goes out of scope (declared before the lock_guard, so
+// after the mutex is released)
+struct Evicted {
+  std::vector<GraphEntry> v;
+  ~Evicted() { graph_entries_destroy(v); }
+};
 
 std::string graph_key(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* ids,
                       int nids, int B, const int* out_ids, const float* logits, const void* ws) {
@@ -399,6 +436,7 @@ std::string graph_key(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const 
 // Replay the graph cached under `key`, capturing `issue(capture_stream)` into it first if absent.
 template <typename Issue>
 int launch_cached(const std::string& key, hipStream_t s, Issue issue) {
+  Evicted evicted;   // destroyed after the lock is released (declared first)
   std::lock_guard<std::mutex> lk(g_graph_mu);
   auto it = g_graphs.find(key);
   if (it == g_graphs.end()) {
@@ -426,7 +464,7 @@ int launch_cached(const std::string& key, hipStream_t s, Issue issue) {
       (void)hipGraphExecDestroy(ge.exec);
       return hip_fail(ee, "hipEventCreate");
     }
-    graph_cache_evict_to(graph_cache_cap() - 1);
+    evicted.v = graph_cache_evict_to(graph_cache_cap() - 1);
     g_graph_lru.push_front(key);
     ge.lru = g_graph_lru.begin();
     it = g_graphs.emplace(key, ge).first;
@@ -747,49 +785,62 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
     const bool last = l == d->depth - 1;
     const int Mt = last ? BT : M;                       // rows after the QKV projection
     const char* probe_attn = last ? "vit.attention.cls" : "vit.attention";
-    if (mx)
+    // MXFP8 mode, per GEMM (weight scales present): the producer of its A operand emits MXFP8
+    const bool mq = mx && ly.qkv_ws, mp = mx && ly.proj_ws, m1 = mx && ly.fc1_ws, m2 = mx && ly.fc2_ws;
+    const int dq = mq ? VCAP_DT_MXFP8 : adt, dp = mp ? VCAP_DT_MXFP8 : adt;
+    const int d1 = m1 ? VCAP_DT_MXFP8 : adt, d2 = m2 ? VCAP_DT_MXFP8 : adt;
+    if (mq)
       VCAP_TRY(vcap_layernorm_mx_dispatch(w.x, D, (uint8_t*)w.xn, w.xn_s, M, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s),
                "norm1");
     else
-      VCAP_TRY(vcap_layernorm_dispatch(dt, w.x, D, w.xn, D, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s), "norm1");
-    GemmEpi e1{ly.qkv_b, nullptr, 0, 0, 0, 0, 0, 0, 0, w.xn_s, ly.qkv_ws, nullptr};
+      VCAP_TRY(vcap_layernorm_dispatch(adt, w.x, D, w.xn, D, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s), "norm1");
+    GemmEpi e1{ly.qkv_b, nullptr, 0, 0, 0, 0, 0, 0, 0, mq ? w.xn_s : nullptr, mq ? ly.qkv_ws : nullptr, nullptr};
     {
-      ProbeScope ps("vit.qkv", s);
-      VCAP_TRY(vcap_gemm_dispatch(dt, adt, w.xn, D, ly.qkv_w, D, w.qkv, 3 * D, M, 3 * D, D, e1, s), "qkv");
+      ProbeScope ps("vit.qkv", s, M);
+      VCAP_TRY(vcap_gemm_dispatch(dq, adt, w.xn, D, ly.qkv_w, D, w.qkv, 3 * D, M, 3 * D, D, e1, s), "qkv");
     }
     {
-      ProbeScope ps(probe_attn, s);
-      if (mx)
+      ProbeScope ps(probe_attn, s, M);
+      if (mp)
         VCAP_TRY(vcap_vit_attention_mx_dispatch(w.qkv, w.attn, w.xn_s, BT, N, d->heads, s, last), "attention");
       else
         VCAP_TRY(vcap_vit_attention_dispatch(adt, w.qkv, w.attn, BT, N, d->heads, s, last), "attention");
     }
     // MXFP8: the attention output arrives as MXFP8 (its scales reuse xn_s, free until norm2)
-    GemmEpi e2{ly.proj_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, w.xn_s, ly.proj_ws, nullptr,
-               last ? w.splitk : nullptr, w.splitk_bytes};
+    GemmEpi e2{ly.proj_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, mp ? w.xn_s : nullptr,
+               mp ? ly.proj_ws : nullptr, nullptr, last ? w.splitk : nullptr, w.splitk_bytes};
     {
-      ProbeScope ps(last ? "vit.proj.cls" : "vit.proj", s);
-      VCAP_TRY(vcap_gemm_dispatch(dt == VCAP_DT_MXFP8 ? dt : adt, VCAP_DT_F32, w.attn, D, ly.proj_w, D, w.x, D, Mt, D,
-                                  D, e2, s),
-               "attn_proj");
+      ProbeScope ps(last ? "vit.proj.cls" : "vit.proj", s, Mt);
+      VCAP_TRY(vcap_gemm_dispatch(dp, VCAP_DT_F32, w.attn, D, ly.proj_w, D, w.x, D, Mt, D, D, e2, s), "attn_proj");
     }
     const long ldx2 = last ? (long)N * D : D;            // CLS rows of x are N*D apart
-    if (mx)
+    if (m1)
       VCAP_TRY(vcap_layernorm_mx_dispatch(w.x, ldx2, (uint8_t*)w.xn, w.xn_s, Mt, ly.ln2_g, ly.ln2_b, Mt, D,
                                           d->ln_eps, s),
                "norm2");
     else
-      VCAP_TRY(vcap_layernorm_dispatch(dt, w.x, ldx2, w.xn, D, ly.ln2_g, ly.ln2_b, Mt, D, d->ln_eps, s), "norm2");
-    GemmEpi e3{ly.fc1_b, nullptr, 0, 1, 0, 0, 0, 0, 0, w.xn_s, ly.fc1_ws, w.act_s};
+      VCAP_TRY(vcap_layernorm_dispatch(adt, w.x, ldx2, w.xn, D, ly.ln2_g, ly.ln2_b, Mt, D, d->ln_eps, s), "norm2");
+    // fc1 emits MXFP8 straight from its epilogue when both MLP GEMMs are MXFP8; an MXFP8 fc2 after
+    // a bf16 fc1 quantises the bf16 activation (vcap_mx_quantize) into the free qkv buffer
+    const bool fused_q = m1 && m2;
+    GemmEpi e3{ly.fc1_b, nullptr, 0, 1, 0, 0, 0, 0, 0, m1 ? w.xn_s : nullptr, m1 ? ly.fc1_ws : nullptr,
+               fused_q ? w.act_s : nullptr};
     {
-      ProbeScope ps(last ? "vit.fc1.cls" : "vit.fc1", s);
-      VCAP_TRY(vcap_gemm_dispatch(dt, dt, w.xn, D, ly.fc1_w, D, w.act, d->mlp, Mt, d->mlp, D, e3, s), "fc1");
+      ProbeScope ps(last ? "vit.fc1.cls" : "vit.fc1", s, Mt);
+      VCAP_TRY(vcap_gemm_dispatch(d1, fused_q ? VCAP_DT_MXFP8 : adt, w.xn, D, ly.fc1_w, D, w.act, d->mlp, Mt, d->mlp,
+                                  D, e3, s),
+               "fc1");
     }
-    GemmEpi e4{ly.fc2_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, w.act_s, ly.fc2_ws, nullptr,
-               last ? w.splitk : nullptr, w.splitk_bytes};
+    const void* a2 = w.act;
+    if (m2 && !fused_q) {
+      VCAP_TRY(vcap_mx_quantize_dispatch(adt, w.act, d->mlp, Mt, d->mlp, (uint8_t*)w.qkv, w.act_s, Mt, s), "fc1 quant");
+      a2 = w.qkv;
+    }
+    GemmEpi e4{ly.fc2_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, m2 ? w.act_s : nullptr,
+               m2 ? ly.fc2_ws : nullptr, nullptr, last ? w.splitk : nullptr, w.splitk_bytes};
     {
-      ProbeScope ps(last ? "vit.fc2.cls" : "vit.fc2", s);
-      VCAP_TRY(vcap_gemm_dispatch(dt, VCAP_DT_F32, w.act, d->mlp, ly.fc2_w, d->mlp, w.x, D, Mt, D, d->mlp, e4, s),
+      ProbeScope ps(last ? "vit.fc2.cls" : "vit.fc2", s, Mt);
+      VCAP_TRY(vcap_gemm_dispatch(d2, VCAP_DT_F32, a2, d->mlp, ly.fc2_w, d->mlp, w.x, D, Mt, D, d->mlp, e4, s),
                "fc2");
     }
   }
@@ -858,6 +909,50 @@ int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const
   });
 }
 
+int vcap_gpt2_sample(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const vcap_sample_params* sp,
+                     const float* prefix, const int* prompt_ids, int prompt_len, int B, int* out_ids,
+                     float* logits_out, float* warped_out, const int* force_ids, void* workspace, size_t ws_bytes,
+                     void* stream) {
+  if (int rc = check_gpt2_launch(d)) return rc;
+  if (!gp || !sp || !prefix || !out_ids || B <= 0 || prompt_len < 0 || prompt_len > 64 || (prompt_len && !prompt_ids))
+    return fail(VCAP_E_ARG, "vcap_gpt2_sample: bad arguments");
+  if (!(sp->temperature > 0.f) || !(sp->top_p > 0.0) || sp->top_p > 1.0 || sp->top_k < 1)
+    return fail(VCAP_E_ARG, "vcap_gpt2_sample: needs temperature > 0, 0 < top_p <= 1, top_k >= 1");
+  if (sp->top_k > vcap_sample_max_top_k() || d->vocab > 50 * 1024)
+    return fail(VCAP_E_UNSUPPORTED, "vcap_gpt2_sample: top_k <= 128 and vocab <= 51200");
+  if (gp->max_new_tokens <= 0 || gp->max_new_tokens > 64)
+    return fail(VCAP_E_UNSUPPORTED, "max_new_tokens must be in 1..64");
+  const int S0 = d->prefix_len + prompt_len;
+  if (B * S0 > kMaxDecodeRows) return fail(VCAP_E_UNSUPPORTED, "B*(prefix+prompt) exceeds vcap_gpt2_max_rows()");
+  if (S0 + gp->max_new_tokens > d->n_positions) return fail(VCAP_E_UNSUPPORTED, "context exceeds n_positions");
+  for (int i = 0; i < prompt_len; ++i)
+    if (prompt_ids[i] < 0 || prompt_ids[i] >= d->vocab) return fail(VCAP_E_ARG, "prompt id out of range");
+  if (ws_bytes < vcap_gpt2_workspace_bytes(d, B, S0, gp->max_new_tokens))
+    return fail(VCAP_E_WORKSPACE, "vcap_gpt2_sample: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  Carver c(workspace);
+  int maxp;
+  size_t page_elems;
+  DecBufs w = carve_dec(c, d, B, S0, gp->max_new_tokens, &maxp, &page_elems);
+  // the Philox key goes to device memory outside the graph: one captured graph serves every seed
+  VCAP_TRY(hipMemsetD32Async((hipDeviceptr_t)w.seed, (int)(uint32_t)sp->seed, 1, s), "seed lo");
+  VCAP_TRY(hipMemsetD32Async((hipDeviceptr_t)(w.seed + 1), (int)(uint32_t)(sp->seed >> 32), 1, s), "seed hi");
+  if (!gp->use_graph)
+    return issue_decode(d, gp, prefix, prompt_ids, prompt_len, B, out_ids, logits_out, w, maxp, page_elems, s, sp,
+                        warped_out, force_ids);
+  std::string key = graph_key(d, gp, prefix, prompt_ids, prompt_len, B, out_ids, logits_out, workspace);
+  vcap_sample_params ks = *sp;
+  ks.seed = 0;
+  key.append("sample");
+  key.append((const char*)&ks, sizeof(ks));
+  key.append((const char*)&warped_out, sizeof(warped_out));
+  key.append((const char*)&force_ids, sizeof(force_ids));
+  return launch_cached(key, s, [&](hipStream_t cs) {
+    return issue_decode(d, gp, prefix, prompt_ids, prompt_len, B, out_ids, logits_out, w, maxp, page_elems, cs, sp,
+                        warped_out, force_ids);
+  });
+}
+
 int vcap_probe_enable(const char* site, int max_launches) {
   if (!site || max_launches <= 0) return fail(VCAP_E_ARG, "vcap_probe_enable: bad arguments");
   std::lock_guard<std::mutex> lk(g_probe_mu);
@@ -868,9 +963,30 @@ int vcap_probe_enable(const char* site, int max_launches) {
     VCAP_TRY(hipEventCreate(&b), "hipEventCreate");
     p.start.push_back(a);
     p.stop.push_back(b);
+    p.rows.push_back(0);
   }
   p.used = 0;
   p.on = true;
+  return 0;
+}
+
+int vcap_probe_read_launches(const char* site, float* ms, int* rows, int cap, int* launches) {
+  if (!site || !launches || cap < 0 || (cap > 0 && (!ms || !rows)))
+    return fail(VCAP_E_ARG, "vcap_probe_read_launches: bad arguments");
+  std::lock_guard<std::mutex> lk(g_probe_mu);
+  auto it = g_probes.find(site);
+  *launches = 0;
+  if (it == g_probes.end()) return 0;
+  Probe& p = it->second;
+  if (p.used > cap) return fail(VCAP_E_ARG, "vcap_probe_read_launches: more launches than cap");
+  for (int i = 0; i < p.used; ++i) {
+    VCAP_TRY(hipEventSynchronize(p.stop[i]), "hipEventSynchronize");
+    VCAP_TRY(hipEventElapsedTime(&ms[i], p.start[i], p.stop[i]), "hipEventElapsedTime");
+    rows[i] = p.rows[i];
+  }
+  *launches = p.used;
+  p.on = false;
+  p.used = 0;
   return 0;
 }
 
@@ -1014,10 +1130,14 @@ int vcap_decode_attention(int dtype, const void* q, const void* k_pool, const vo
 }
 
 void vcap_graph_cache_clear(void) {
-  std::lock_guard<std::mutex> lk(g_graph_mu);
-  graph_cache_evict_to(0);
-  g_graphs.clear();
-  g_graph_lru.clear();
+  std::vector<GraphEntry> evicted;
+  {
+    std::lock_guard<std::mutex> lk(g_graph_mu);
+    evicted = graph_cache_evict_to(0);
+    g_graphs.clear();
+    g_graph_lru.clear();
+  }
+  graph_entries_destroy(evicted);
 }
 
 int vcap_gpt2_max_rows(void) { return kMaxDecodeRows; }

@@ -56,7 +56,27 @@ struct RowsGemmArgs {
   float rep_penalty;
   int min_new, eos;
   int max_blocks;  // 0: one 16-column tile per workgroup; > 0: widen tiles to stay near this grid
+  float* proc_out;  // EPI_LOGITS, optional [M, N]: the processed scores (sampling mode)
 };
+
+// ---- sampling warpers + draw (csrc/sample.hip)
+struct SampleArgs {
+  const float* proc;  // [rows][ldp] processed scores (processors applied)
+  int V, ldp;
+  float temperature;
+  int top_k;
+  double top_p;
+  const unsigned* seed;  // device [2]: Philox key
+  int step;
+  const int* force;      // optional [rows][force_ld]: emit these tokens instead of drawing (tests)
+  int force_ld;
+  float* warped;         // optional [rows][warped_ld]: the warped scores HF's _sample draws from
+  long warped_ld;
+  float* pval;           // [rows]: the token as the finalize kernel's only argmax partial
+  int* pidx;
+};
+hipError_t vcap_sample_dispatch(const SampleArgs& a, int rows, hipStream_t s);
+int vcap_sample_max_top_k();
 
 hipError_t vcap_gemm_dispatch(int in_dt, int out_dt, const void* A, long lda, const void* W, long ldw, void* C,
                               long ldc, int M, int N, int K, const GemmEpi& epi, hipStream_t s);

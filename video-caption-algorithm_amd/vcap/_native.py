@@ -16,14 +16,19 @@ _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
 DT_F32, DT_BF16, DT_MXFP8 = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 8
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
 
 
+E_ARG, E_WORKSPACE, E_UNSUPPORTED = -1000, -1001, -1002
+
+
 class VcapError(RuntimeError):
-    pass
+    def __init__(self, msg: str, rc: int = 0):
+        super().__init__(msg)
+        self.rc = rc
 
 
 class VitLayer(C.Structure):
@@ -67,6 +72,10 @@ class BeamParams(C.Structure):
                 ("early_stopping", i32), ("eos_token_id", i32), ("use_graph", i32)]
 
 
+class SampleParams(C.Structure):
+    _fields_ = [("temperature", f32), ("top_k", i32), ("top_p", C.c_double), ("seed", C.c_uint64)]
+
+
 # name -> (restype, argtypes); every symbol include/vcap.h declares
 SIGNATURES = {
     "vcap_last_error": (C.c_char_p, []),
@@ -96,6 +105,8 @@ SIGNATURES = {
     "vcap_gpt2_workspace_bytes": (sz, [C.POINTER(GPT2Desc), i32, i32, i32]),
     "vcap_gpt2_generate": (i32, [C.POINTER(GPT2Desc), C.POINTER(GenParams), vp, C.POINTER(C.c_int), i32, i32, vp,
                                  vp, vp, sz, vp]),
+    "vcap_gpt2_sample": (i32, [C.POINTER(GPT2Desc), C.POINTER(GenParams), C.POINTER(SampleParams), vp,
+                               C.POINTER(C.c_int), i32, i32, vp, vp, vp, vp, vp, sz, vp]),
     "vcap_graph_cache_clear": (None, []),
     "vcap_graph_cache_size": (i32, []),
     "vcap_gpt2_max_rows": (i32, []),
@@ -110,6 +121,7 @@ SIGNATURES = {
     "vcap_gpt2_forward_embeds": (i32, [C.POINTER(GPT2Desc), vp, i32, i32, i32, i32, i32, vp, vp, sz, vp]),
     "vcap_probe_enable": (i32, [C.c_char_p, i32]),
     "vcap_probe_read": (i32, [C.c_char_p, fp, C.POINTER(C.c_int)]),
+    "vcap_probe_read_launches": (i32, [C.c_char_p, fp, C.POINTER(C.c_int), i32, C.POINTER(C.c_int)]),
 }
 
 
@@ -140,7 +152,7 @@ def lib():
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = lib().vcap_last_error()
-        raise VcapError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+        raise VcapError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}", rc)
 
 
 def ptr(t) -> int:

@@ -13,7 +13,8 @@ plus the batched fast path `generate_ids(video, prompt_ids, ...)` -> int32 [B, m
 
 Decode semantics of decoder.generate (text_decoder.py:131-144): num_beams == 1 and temperature == 1
 -> greedy with RepetitionPenalty, NoRepeatNGram and min_new_tokens (on device, one hipGraph);
-num_beams > 1 -> beam search; num_beams == 1 and temperature != 1 -> sampling (temperature, top-p).
+num_beams > 1 -> beam search; num_beams == 1 and temperature != 1 -> sampling (temperature, top-k 50,
+top-p; on device, one hipGraph).
 """
 from __future__ import annotations
 
@@ -158,7 +159,7 @@ class HipTextDecoder:
             return trim_generated(ids, eos)
         from . import search
         if num_beams > 1:
-            return search.beam_search_device(self.hip, prefix, prompt_ids, num_beams=num_beams,
+            return search.beam_search_any(self.hip, prefix, prompt_ids, num_beams=num_beams,
                                              max_new_tokens=max_new_tokens, min_new_tokens=min_new_tokens,
                                              no_repeat_ngram_size=no_repeat_ngram_size,
                                              repetition_penalty=repetition_penalty, eos=eos,
@@ -166,7 +167,7 @@ class HipTextDecoder:
         return search.sample(self.hip, prefix, prompt_ids, temperature=temperature, top_p=top_p,
                              max_new_tokens=max_new_tokens, min_new_tokens=min_new_tokens,
                              no_repeat_ngram_size=no_repeat_ngram_size, repetition_penalty=repetition_penalty,
-                             eos=eos, seed=seed)
+                             eos=eos, seed=seed, use_graph=self.use_graph)
 
     @torch.no_grad()
     def generate(self, video_emb: torch.Tensor, prompt: str = "", max_new_tokens: int = 32, num_beams: int = 1,

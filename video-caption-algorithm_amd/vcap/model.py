@@ -53,14 +53,22 @@ class _Workspace:
 class HipViTEncoder:
     """ViTFrameEncoder.forward (src/models/video_encoder.py:288-326) on the HIP path."""
 
+    MX_GEMMS = ("qkv", "proj", "fc1", "fc2")
+
     def __init__(self, sd: Dict[str, np.ndarray], arch: ViTArch, precision: str = "bf16", device="cuda",
-                 video_dim: int = VIDEO_DIM):
+                 video_dim: int = VIDEO_DIM, mx_gemms: Sequence[str] = MX_GEMMS):
+        """precision "fp8": the block GEMMs named in `mx_gemms` run in MXFP8, the others in bf16
+        (their weights bf16, their scales NULL in the descriptor: csrc/runtime.hip picks per GEMM)."""
         N.lib()
         self.arch, self.precision, self.device = arch, precision, torch.device(device)
         if precision not in _VIT_DTYPES:
             raise ValueError(f"precision must be one of {sorted(_VIT_DTYPES)}, got {precision!r}")
+        bad = set(mx_gemms) - set(self.MX_GEMMS)
+        if bad:
+            raise ValueError(f"mx_gemms: unknown GEMM(s) {sorted(bad)}; choose from {self.MX_GEMMS}")
         self.dt, tdt = _VIT_DTYPES[precision]
         mx = self.dt == N.DT_MXFP8
+        self.mx_gemms = tuple(g for g in self.MX_GEMMS if g in mx_gemms) if mx else ()
         self.video_dim = video_dim
         p = "encoder.backbone."
         dev = self.device
@@ -111,7 +119,7 @@ class HipViTEncoder:
                       fc1_b=f32(b + "mlp.fc1.bias"), fc2_b=f32(b + "mlp.fc2.bias"))
             for name, key in (("qkv", "attn.qkv.weight"), ("proj", "attn.proj.weight"), ("fc1", "mlp.fc1.weight"),
                               ("fc2", "mlp.fc2.weight")):
-                if mx:
+                if name in self.mx_gemms:
                     lt[name + "_w"], lt[name + "_ws"] = wmx(b + key)
                 else:
                     lt[name + "_w"] = wt(b + key)
@@ -205,6 +213,16 @@ class GenConfig:
     max_blocks: int = 0      # >0: narrower decode grids (decode sharing the GPU with an encode)
     num_beams: int = 1       # >1: device beam search (vcap_gpt2_beam_search, presets precise / detailed)
     length_penalty: float = 1.0
+    # sampling (presets natural / safe_sample): HF's do_sample = (num_beams == 1 and temperature != 1),
+    # text_decoder.py:137; top_k 50 is the generation-config default the reference inherits
+    temperature: float = 1.0
+    top_k: int = 50
+    top_p: float = 1.0
+    seed: int = 0
+
+    @property
+    def do_sample(self) -> bool:
+        return self.num_beams == 1 and self.temperature != 1.0
 
     @classmethod
     def raw_greedy(cls, max_new_tokens: int = 24, eos: int = 50256, use_graph: bool = True) -> "GenConfig":
@@ -278,7 +296,8 @@ class HipGPT2Decoder:
 
     def generate_ids(self, prefix: torch.Tensor, prompt_ids: Sequence[int], cfg: GenConfig,
                      out: Optional[torch.Tensor] = None, logits_out: Optional[torch.Tensor] = None,
-                     workspace: Optional["_Workspace"] = None, lengths_out: Optional[torch.Tensor] = None
+                     workspace: Optional["_Workspace"] = None, lengths_out: Optional[torch.Tensor] = None,
+                     warped_out: Optional[torch.Tensor] = None, force_ids: Optional[torch.Tensor] = None
                      ) -> torch.Tensor:
         """prefix [B,P,E] f32 device, prompt ids (BOS-only prompt = [eos]) -> int32 [B, max_new] EOS-padded.
 
@@ -294,7 +313,8 @@ class HipGPT2Decoder:
         prefix = prefix.to(torch.float32).contiguous()
         ids = list(int(i) for i in prompt_ids)
         mx = int(cfg.max_new_tokens)
-        fresh = out is None and logits_out is None and workspace is None and cfg.use_graph
+        fresh = (out is None and logits_out is None and workspace is None and warped_out is None and force_ids is None
+                 and cfg.use_graph)
         if fresh:
             # A replayed graph bakes in the prefix / ids addresses: a caller that hands over new
             # tensors every call (the engine path) decodes through persistent per-shape buffers,
@@ -311,6 +331,8 @@ class HipGPT2Decoder:
             out = torch.empty(B, mx, dtype=torch.int32, device=prefix.device)
         if logits_out is not None and tuple(logits_out.shape) != (mx, B, self.arch.vocab):
             raise ValueError("logits_out must be [max_new, B, vocab] f32")
+        if (warped_out is not None or force_ids is not None) and not cfg.do_sample:
+            raise ValueError("warped_out / force_ids belong to the sampling mode (temperature != 1)")
         gp = N.GenParams(max_new_tokens=mx, min_new_tokens=int(cfg.min_new_tokens),
                          no_repeat_ngram_size=int(cfg.no_repeat_ngram_size),
                          repetition_penalty=float(cfg.repetition_penalty), eos_token_id=int(cfg.eos_token_id),
@@ -318,6 +340,21 @@ class HipGPT2Decoder:
                          max_blocks=int(cfg.max_blocks))
         arr = (C.c_int * max(len(ids), 1))(*ids)
         ws = (workspace or self.ws).get(self.workspace_bytes(B, len(ids), mx))
+        if cfg.do_sample:
+            if warped_out is not None and (tuple(warped_out.shape) != (mx, B, self.arch.vocab)
+                                           or warped_out.dtype != torch.float32 or not warped_out.is_contiguous()):
+                raise ValueError("warped_out must be contiguous f32 [max_new, B, vocab]")
+            if force_ids is not None:
+                if tuple(force_ids.shape) != (B, mx):
+                    raise ValueError("force_ids must be [B, max_new]")
+                force_ids = force_ids.to(device=prefix.device, dtype=torch.int32).contiguous()
+            sp = N.SampleParams(temperature=float(cfg.temperature), top_k=int(cfg.top_k), top_p=float(cfg.top_p),
+                                seed=int(cfg.seed) & 0xFFFFFFFFFFFFFFFF)
+            N.check(N.lib().vcap_gpt2_sample(C.byref(self.desc), C.byref(gp), C.byref(sp), prefix.data_ptr(), arr,
+                                             len(ids), B, out.data_ptr(), N.ptr(logits_out), N.ptr(warped_out),
+                                             N.ptr(force_ids), ws.data_ptr(), ws.numel(), _stream(prefix.device)),
+                    "vcap_gpt2_sample")
+            return out
         N.check(N.lib().vcap_gpt2_generate(C.byref(self.desc), C.byref(gp), prefix.data_ptr(), arr, len(ids), B,
                                            out.data_ptr(), N.ptr(logits_out), ws.data_ptr(), ws.numel(),
                                            _stream(prefix.device)), "vcap_gpt2_generate")

@@ -88,6 +88,11 @@ class CaptionPipeline:
             else:
                 self.s_decs = [torch.cuda.Stream(self.device, priority=hi) for _ in range(self.lanes)]
         self.s_dec = self.s_decs[0]
+        # the encoder / decoder workspaces are shared with serial calls made on the creating stream:
+        # nothing of the pipeline may start before that stream's pending work has finished
+        cur = torch.cuda.current_stream(self.device)
+        for st in [self.s_enc] + self.s_decs:
+            st.wait_stream(cur)
         self.dec_ws = [decoder.ws] + [_Workspace(self.device) for _ in range(self.lanes - 1)]
         E = decoder.arch.n_embd
         G = self.group

@@ -12,7 +12,8 @@ text_decoder.py:131-144 with inputs_embeds (decoder_prompt_len = 0): log_softmax
 (RepetitionPenalty, NoRepeatNGram, MinLength/MinNewTokens) -> + running scores -> top-2k over
 beams x vocab -> running / finished beam updates with length_penalty=1.0, early_stopping=False
 -> cache reorder.  Sampling restates `_sample` with TemperatureLogitsWarper + TopKLogitsWarper(50) + TopPLogitsWarper;
-its RNG stream is torch's, so parity with the reference is distributional only.
+it runs on the device (csrc/sample.hip); its RNG stream is Philox, so parity with the reference is
+distributional only; `sampling_scores` is the torch restatement of the warped scores (test reference).
 """
 from __future__ import annotations
 
@@ -80,6 +81,45 @@ def beam_search_device(dec, prefix: torch.Tensor, prompt_ids: Sequence[int], *, 
     ids = out.cpu()
     n = int(lens.max().item())
     return [list(map(int, r)) for r in ids[:, :n].tolist()]
+
+
+BEAM_DEVICE_MAX_B = 8   # sequences per device beam-search call (csrc/beam.hip select kernel: one wave each)
+
+
+@torch.no_grad()
+def beam_search_any(dec, prefix: torch.Tensor, prompt_ids: Sequence[int], *, num_beams: int, max_new_tokens: int,
+                    min_new_tokens: int = 8, no_repeat_ngram_size: int = 3, repetition_penalty: float = 1.1,
+                    eos: int = 50256, length_penalty: float = 1.0, use_graph: bool = True) -> List[List[int]]:
+    """Beam search for any batch: sequences go to the device search (one hipGraph) in chunks within
+    its limits (<= 8 sequences, B * num_beams * (prefix + prompt) <= vcap_gpt2_max_rows()); a shape
+    the device search refuses (num_beams > 8 or too many candidates for the vocabulary, context
+    > 128) runs the host-bookkeeping search over the same step kernels.  Sequences are independent
+    in HF's search, so chunking changes nothing but the padding: rows are EOS-padded to the longest
+    hypothesis of the whole batch, as one generate() call returns them."""
+    B = prefix.shape[0]
+    S0 = dec.prefix_len + len(prompt_ids)
+    limit = int(N.lib().vcap_gpt2_max_rows())
+    step = max(1, min(BEAM_DEVICE_MAX_B, limit // max(1, num_beams * S0)))
+    kw = dict(num_beams=num_beams, max_new_tokens=max_new_tokens, min_new_tokens=min_new_tokens,
+              no_repeat_ngram_size=no_repeat_ngram_size, repetition_penalty=repetition_penalty, eos=eos,
+              length_penalty=length_penalty)
+    rows: List[List[int]] = []
+    device_ok = True
+    for i in range(0, B, step):
+        chunk = prefix[i:i + step]
+        if device_ok:
+            try:
+                rows += beam_search_device(dec, chunk, prompt_ids, use_graph=use_graph, **kw)
+                continue
+            except N.VcapError as e:
+                if e.rc != N.E_UNSUPPORTED:
+                    raise
+                device_ok = False
+        host_step = max(1, min(chunk.shape[0], limit // max(1, num_beams), limit // max(1, S0)))
+        for j in range(0, chunk.shape[0], host_step):
+            rows += beam_search(dec, chunk[j:j + host_step], prompt_ids, **kw)
+    width = max(len(r) for r in rows)
+    return [r + [eos] * (width - len(r)) for r in rows]
 
 
 def _processors(scores: torch.Tensor, seqs: torch.Tensor, rep: float, ngram: int, min_new: int, eos: int):
@@ -214,22 +254,14 @@ def sampling_scores(logits: torch.Tensor, seqs: torch.Tensor, *, temperature: fl
 @torch.no_grad()
 def sample(dec, prefix: torch.Tensor, prompt_ids: Sequence[int], *, temperature: float, top_p: float,
            max_new_tokens: int, min_new_tokens: int = 8, no_repeat_ngram_size: int = 3,
-           repetition_penalty: float = 1.1, eos: int = 50256, seed: int = 0) -> List[List[int]]:
-    B, dev = prefix.shape[0], prefix.device
-    S0 = dec.prefix_len + len(prompt_ids)
-    st = _StepState(dec, B, S0, max_new_tokens)
-    logits = st.prefill(prefix, list(prompt_ids))
-    gen = torch.Generator(device=dev).manual_seed(int(seed))
-    seqs = torch.zeros(B, 0, dtype=torch.long, device=dev)
-    unfinished = torch.ones(B, dtype=torch.bool, device=dev)
-    for cur in range(max_new_tokens):
-        sc = sampling_scores(logits, seqs, temperature=temperature, top_p=top_p, rep=repetition_penalty,
-                             ngram=no_repeat_ngram_size, min_new=min_new_tokens, eos=eos)
-        nxt = torch.multinomial(F.softmax(sc, dim=-1), num_samples=1, generator=gen).squeeze(1)
-        nxt = torch.where(unfinished, nxt, torch.full_like(nxt, eos))
-        seqs = torch.cat([seqs, nxt[:, None]], dim=1)
-        unfinished = unfinished & (nxt != eos)
-        if not bool(unfinished.any()) or cur + 1 == max_new_tokens:
-            break
-        logits = st.step(nxt, S0 + cur)
-    return [list(map(int, r)) for r in seqs.cpu().tolist()]
+           repetition_penalty: float = 1.1, eos: int = 50256, seed: int = 0, top_k: int = HF_TOP_K,
+           use_graph: bool = True) -> List[List[int]]:
+    """HF `_sample` on the device (csrc/sample.hip through vcap_gpt2_sample: the greedy graph's
+    processors, then Temperature -> TopK -> TopP and a Philox draw per row and step, one hipGraph,
+    no host sync per token); rows cut where HF's stopping criteria end the batch."""
+    from .model import GenConfig, trim_generated
+    cfg = GenConfig(max_new_tokens, min_new_tokens, no_repeat_ngram_size, repetition_penalty, eos, eos, use_graph,
+                    temperature=temperature, top_k=top_k, top_p=top_p, seed=seed)
+    if not cfg.do_sample:
+        raise ValueError("sampling needs temperature != 1 (HF do_sample rule, text_decoder.py:137)")
+    return trim_generated(dec.generate_ids(prefix, list(prompt_ids), cfg), eos)

@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--max-new", type=int, default=24)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp8"],
                     help="fp8: MXFP8 ViT QKV/fc1/fc2 GEMMs (BASELINE configs[4]); the decoder stays bf16")
+    ap.add_argument("--mx-gemms", default="qkv,proj,fc1,fc2",
+                    help="--precision fp8: the ViT block GEMMs run in MXFP8 (the others bf16)")
     ap.add_argument("--decode", default="hf_greedy", choices=["hf_greedy", "raw_greedy"])
     ap.add_argument("--beams", type=int, default=1,
                     help=">1: device beam search (preset detailed = 4 beams / max_new 40: BASELINE configs[3])")
@@ -74,6 +76,8 @@ def parse():
                     help="consecutive batches encoded together as one encode (divides --dec-group); 0 = auto: "
                          "2 while a batch holds <= 128 frames (the N = 768 GEMMs of one 8 x 16-frame batch fill "
                          "1.16 rounds of 256 tiles), else 1")
+    ap.add_argument("--decode-priority", default="high", choices=["high", "normal"],
+                    help="stream priority of the decode lanes (the encode stream is normal)")
     ap.add_argument("--confine-decode", action="store_true",
                     help="mask the decode streams to the reserved CUs (default: unmasked, high priority)")
     ap.add_argument("--gemm-policy", type=int, default=0, help="vcap_set_gemm_policy value for A/B runs (0 = auto)")
@@ -300,7 +304,8 @@ def main():
     video = torch.from_numpy(frames_np).to(dev)
 
     N.check(N.lib().vcap_set_gemm_policy(args.gemm_policy), "gemm policy")
-    enc = HipViTEncoder(sd, va, args.precision, dev)
+    mx_gemms = tuple(g for g in args.mx_gemms.split(",") if g)
+    enc = HipViTEncoder(sd, va, args.precision, dev, mx_gemms=mx_gemms)
     pre = HipPrefix(sd, ga.n_embd, device=dev)
     dec = HipGPT2Decoder(sd, ga, "bf16" if args.precision == "fp8" else args.precision, dev)
     if args.decode == "hf_greedy":
@@ -325,6 +330,7 @@ def main():
                            reserve_cus=0 if args.serial else args.reserve_cus,
                            dec_lanes=1 if args.serial else args.dec_lanes,
                            confine_decode=args.confine_decode and not args.serial,
+                           decode_priority=args.decode_priority,
                            dec_group=1 if args.serial else args.dec_group,
                            enc_group=1 if args.serial else args.enc_group)
 
@@ -450,7 +456,7 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "captions/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": {"bf16": "bf16", "fp8": "mxfp8-e4m3 (ViT QKV/proj/fc1/fc2) + bf16"}.get(args.precision, "f32"),
+            "scaling": "weak", "vs_baseline": None, "dtype": {"bf16": "bf16", "fp8": f"mxfp8-e4m3 (ViT {'/'.join(enc.mx_gemms)}) + bf16"}.get(args.precision, "f32"),
             "data": "synthetic (seeded U[0,1) frames, ImageNet-normalised; seeded random-init weights)",
             "config": {"workload": f"batch={B} synthetic {T}x3x224x224 videos per GPU, {args.vit} + {args.gpt2}, "
                                    f"{args.decode if args.beams == 1 else f'beam-{args.beams}'} decode max_new {args.max_new} "

@@ -1,6 +1,7 @@
 """One rank of the data-parallel caption path (vcap.dist.caption_sharded), started as a child
 process by tests/test_gpu_dist.py (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the env).
-Both ranks share the box's one GPU and talk over gloo; rank 0 writes the gathered ids as JSON."""
+Both ranks share the box's one GPU and talk over gloo (or one rank over RCCL: the box has one GPU);
+rank 0 writes the gathered ids as JSON."""
 import json
 import os
 import sys
@@ -13,13 +14,18 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
-def main(case_name: str, out_path: str) -> None:
+def main(case_name: str, out_path: str, backend: str = "gloo") -> None:
     from helpers import case
     from vcap.caption import HipVideoCaptionModel
     from vcap.dist import caption_sharded
     from vcap.model import GenConfig
 
-    dist.init_process_group("gloo")
+    dev0 = torch.device("cuda", 0)
+    if backend == "nccl":   # RCCL: one rank per GPU (the box has one: world size 1)
+        torch.cuda.set_device(dev0)
+        dist.init_process_group("nccl", device_id=dev0)
+    else:
+        dist.init_process_group(backend)
     meta, g, va, ga, sd, frames = case(case_name)
     dev = torch.device("cuda", 0)
     model = HipVideoCaptionModel(sd, meta["vit"], meta["gpt2"], 4, "fp32", dev)
@@ -34,4 +40,4 @@ def main(case_name: str, out_path: str) -> None:
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *(sys.argv[3:4]))

@@ -51,6 +51,24 @@ def test_caption_sharded_two_ranks_match_goldens(tmp_path, name):
     assert (got[:, exp.shape[1]:] == eos).all()
 
 
+def test_caption_sharded_rccl_one_rank(tmp_path):
+    """The RCCL branch of vcap.dist.gather_ids ("nccl" backend: all_gather_into_tensor on the
+    device) executed for real: one rank per GPU on this one-GPU box, world size 1; the ids equal
+    the reference's goldens."""
+    name = "tiny_prompt"
+    out = tmp_path / "ids.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="1", RANK="0",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(HERE / "dist_worker.py"), name, str(out), "nccl"], env=env,
+                       capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    res = json.loads(out.read_text())
+    meta, g = golden(name)
+    got = np.array(res["ids"], dtype=np.int32)
+    exp = g["hf_greedy_ids"]
+    assert res["world"] == 1 and np.array_equal(got[:, :exp.shape[1]], exp)
+
+
 def test_bench_two_ranks_gloo(tmp_path):
     """The N>1 bench path (torchrun, one process per rank, sharded videos, decode-lane id copies,
     ONE end-of-run all-gather, MAX-over-ranks timing) rehearsed with 2 ranks sharing the box's

@@ -56,9 +56,6 @@ __global__ __launch_bounds__(256) void vcap_rows_pack_kernel(const T* __restrict
 }
 
 VCAP_DEV const u32x4* packed_frag(const void* w, int tile, int nslab, int slab, int lane) {
-#ifdef VCAP_DIAG_W0   // diagnostic build only: every workgroup reads tile 0's weights (L2-resident)
-  tile = 0;
-#endif
   return reinterpret_cast<const u32x4*>(w) + ((long)tile * nslab + slab) * 64 + lane;
 }
 
@@ -832,7 +829,9 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
   return launch_generic<T, MT, NTB, PRO, EPI>(a, s);
 }
 
-// 16-column tiles per workgroup: the lm_head always takes 4 (argmax partials per 64 columns);
+// 16-column tiles per workgroup: the lm_head always takes 4 (argmax partials per 64 columns; 786
+// workgroups at 2 per CU.  r03: 5 or 8 tiles per workgroup (629 / 393 workgroups) measured +6 / +8 us
+// per token step, and forcing 3 workgroups per CU (<= 168 VGPRs) +22 us);
 // the projections take 1 unless a grid cap asks for wider workgroups (2 or 4 tiles).
 static int rows_ntb(int epi, int N = 0, int max_blocks = 0) {
   if (epi == EPI_LOGITS || epi == EPI_LSE) return 4;

@@ -90,22 +90,6 @@ VCAP_DEV void lds_fence() { asm volatile("" ::: "memory"); }
 
 }  // namespace
 
-#ifdef VCAP_GEMM_STAMPS
-// Diagnostic build only (tools/gemm_stamps.py): per workgroup, wave 0 records the 100 MHz real
-// time at entry, after the prologue's first K-tile landed, after the K loop, after its epilogue
-// stores were issued and after they completed, plus its XCC / hardware id.  No output value is
-// computed from these.
-constexpr int kStampWgs = 8192;
-__device__ unsigned long long vcap_gemm_stamps[kStampWgs * 8];
-extern "C" int vcap_diag_gemm_stamps(void* dst, long bytes) {
-  const long n = bytes < (long)sizeof(vcap_gemm_stamps) ? bytes : (long)sizeof(vcap_gemm_stamps);
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(vcap_gemm_stamps), n, 0, hipMemcpyDeviceToHost);
-}
-VCAP_DEV unsigned long long stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
-#define VCAP_STAMP(var) const unsigned long long var = stamp_now()
-#else
-#define VCAP_STAMP(var)
-#endif
 
 // Epilogue of a 256-row tile: wave (wr, wc) holds the 128 x 64 block at rows m0 + wr*128, columns
 // n0 + wc*64 as four 64 x 32 quadrants; lane holds C[m][n .. n+3] of each 16x16 MFMA tile
@@ -201,7 +185,7 @@ VCAP_DEV void epilogue256(const f32x4 (&acc)[2][2][4][2], int m0, int n0, int wr
     // quadrant ahead of the stores that follow it in program order: written as load / add / store
     // per element, the loads could not move above the previous element's store (same pointer),
     // and the in-order vmcnt made every load wait for that store too - 32 serialised HBM round
-    // trips per wave, 17.6 us of a 38 us proj tile (tools/gemm_stamps.py).  Rows past M load row
+    // trips per wave, 17.6 us of a 38 us proj tile (r02 per-workgroup stamps, profiles/r02_gemm_stamps.txt).  Rows past M load row
     // M - 1 and store nothing.
     f32x4 bias[2][2];
 #pragma unroll
@@ -425,7 +409,6 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
   };
 
   const int nk = K / BK;  // even, >= 2 (dispatcher)
-  VCAP_STAMP(t_entry);
   // prologue: K-tile 0 complete; K-tile 1 minus its A-h1 in flight
   stA(0, 0);
   stA(1, 0);
@@ -436,7 +419,6 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
   stB(1, 1);
   wait_landed();
   end_phase();
-  VCAP_STAMP(t_landed);
   // Stagger: the wr == 1 wave group runs one barrier behind, so on every SIMD one wave issues
   // its MFMAs while the other issues ds_reads / LDS-DMA.  (Balanced by wr == 0 after the loop.)
   if (wr == 1) __builtin_amdgcn_s_barrier();
@@ -505,28 +487,8 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();
   if constexpr (MX) mfma_mx_drain();
-  VCAP_STAMP(t_kloop);
 
   epilogue256<TIn, TOut, EPI>(acc, m0, n0, wr, wc, lane, M, N, C, ldc, epi);
-#ifdef VCAP_GEMM_STAMPS
-  VCAP_STAMP(t_issued);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  VCAP_STAMP(t_done);
-  if (tid == 0 && bid < kStampWgs) {
-    unsigned xcc, hwid;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-    unsigned long long* o = vcap_gemm_stamps + (long)bid * 8;
-    o[0] = t_entry;
-    o[1] = t_landed;
-    o[2] = t_kloop;
-    o[3] = t_issued;
-    o[4] = t_done;
-    o[5] = ((unsigned long long)xcc << 32) | hwid;
-    o[6] = (unsigned long long)wgid;
-    o[7] = 0;
-  }
-#endif
 }
 
 template <typename TIn, typename TOut, int EPI>

@@ -225,21 +225,9 @@ int check_gpt2_launch(const vcap_gpt2_desc* d) {
   return 0;
 }
 
-// Diagnostic (timing experiments only; results are garbage when set): VCAP_DECODE_DUP bitmask
-// launches a decode kernel twice (1 c_attn, 2 attention, 4 attn c_proj, 8 c_fc, 16 mlp c_proj)
-// so its marginal cost in the dependent chain can be read from the step time.
-int decode_dup_mask() {
-  static int m = [] {
-    const char* e = std::getenv("VCAP_DECODE_DUP");
-    return e ? (int)std::strtol(e, nullptr, 0) : 0;
-  }();
-  return m;
-}
-
 int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_elems, int M, int S_new, int past,
                int max_blocks, hipStream_t s, const int* anc = nullptr, int anc_ld = 0) {
   const int E = d->n_embd, H = d->n_head, L = d->n_layer;
-  const int dup = S_new == 1 ? decode_dup_mask() : 0;
   const int dt = d->dtype;
   const size_t es = esize(dt);
   for (int l = 0; l < L; ++l) {
@@ -257,40 +245,35 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     // pages are allocated contiguously per sequence (identity table written by vcap_decode_init):
     // the scatter computes page ids instead of loading them (nullptr table)
     a.page_table = nullptr; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past; a.max_blocks = max_blocks;
-    for (int r = 0; r < 1 + (dup & 1); ++r) VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
+    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
     // 2) causal attention over the paged cache
     // pages are allocated contiguously per sequence (vcap_decode_init: identity table), so the bf16
     // short-context kernel computes page ids instead of loading them (nullptr table)
     const int* pt_arg = (dt == VCAP_DT_BF16 && past + S_new <= 64) ? nullptr : w.pt;
-    for (int r = 0; r < 1 + ((dup >> 1) & 1); ++r) {
-      if (anc)   // beam search: keys through the ancestry table (one query row per sequence)
-        VCAP_TRY(vcap_decode_attention_anc_dispatch(dt, w.q, a.kc, a.vc, anc, anc_ld, maxp, w.attn, M, H, past, s),
-                 "decode_attention_anc");
-      else
-        VCAP_TRY(vcap_decode_attention_dispatch(dt, w.q, a.kc, a.vc, pt_arg, maxp, w.attn, M, H, S_new, past, s),
-                 "decode_attention");
-    }
+    if (anc)   // beam search: keys through the ancestry table (one query row per sequence)
+      VCAP_TRY(vcap_decode_attention_anc_dispatch(dt, w.q, a.kc, a.vc, anc, anc_ld, maxp, w.attn, M, H, past, s),
+               "decode_attention_anc");
+    else
+      VCAP_TRY(vcap_decode_attention_dispatch(dt, w.q, a.kc, a.vc, pt_arg, maxp, w.attn, M, H, S_new, past, s),
+               "decode_attention");
     // 3) attn c_proj + residual
     RowsGemmArgs b;
     memset(&b, 0, sizeof(b));
     b.M = M; b.x = w.attn; b.ldx = E; b.w = ly.aproj_w; b.bias = ly.aproj_b; b.N = E; b.K = E;
     b.out = w.h; b.ldo = E; b.max_blocks = max_blocks;
-    for (int r = 0; r < 1 + ((dup >> 2) & 1); ++r)
-      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, b, nullptr, s), "attn_c_proj");
+    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, b, nullptr, s), "attn_c_proj");
     // 4) ln_2 + c_fc + gelu_new
     RowsGemmArgs c;
     memset(&c, 0, sizeof(c));
     c.M = M; c.x = w.h; c.ldx = E; c.ln_g = ly.ln2_g; c.ln_b = ly.ln2_b; c.ln_eps = d->ln_eps;
     c.w = ly.fc_w; c.bias = ly.fc_b; c.N = 4 * E; c.K = E; c.out = w.act; c.ldo = 4 * E; c.max_blocks = max_blocks;
-    for (int r = 0; r < 1 + ((dup >> 3) & 1); ++r)
-      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_GELU, c, nullptr, s), "c_fc");
+    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_GELU, c, nullptr, s), "c_fc");
     // 5) mlp c_proj + residual
     RowsGemmArgs e;
     memset(&e, 0, sizeof(e));
     e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.bias = ly.mproj_b; e.N = E;
     e.K = 4 * E; e.out = w.h; e.ldo = E; e.max_blocks = max_blocks;
-    for (int r = 0; r < 1 + ((dup >> 4) & 1); ++r)
-      VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, e, nullptr, s), "mlp_c_proj");
+    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, e, nullptr, s), "mlp_c_proj");
   }
   return 0;
 }
@@ -574,7 +557,7 @@ int vcap_stream_create_cu_reserved(int reserve_cus, void** stream) {
   if (reserve_cus >= ncu) return fail(VCAP_E_ARG, "cannot reserve every CU");
   // Clearing the first `reserve_cus` mask bits: with 32 cleared, the stream's workgroups still land on
   // all 8 XCCs and block id % 8 still picks one XCC, so the GEMMs' XCD-aware tile remap
-  // holds (tools/gemm_stamps.py with RESERVE=32, profiles/r02_encode_alone.txt).
+  // holds (r02 per-workgroup stamps with 32 CUs reserved, profiles/r02_encode_alone.txt).
   std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
   for (int c = reserve_cus; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
   hipStream_t s = nullptr;

@@ -172,13 +172,6 @@ __global__ __launch_bounds__(256) void vcap_vit_attention_kernel(const T* __rest
 // operand that overwrites the source-C registers of an MFMA still in flight.)
 VCAP_DEV float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 
-// minimum waves per SIMD the per-(frame, head) kernel is compiled for at the ViT-B/16 shape (KT = 14).
-// 1 = no register constraint (90 VGPRs, two 8-wave workgroups per CU).  6 would fit three workgroups
-// per CU beside the 53 KiB K / V images (80 VGPRs, the second tile's Q fragments in scratch) and
-// measured 5-10 % slower (profiles/r02_attention_sum_mfma_ab.txt).
-#ifndef VCAP_ATTN_WAVES_PER_SIMD
-#define VCAP_ATTN_WAVES_PER_SIMD 1
-#endif
 
 VCAP_DEV void glds16_attn(const void* g, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -228,16 +221,10 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
 #pragma unroll
     for (int r = 0; r < 4; ++r) st[kt][r] = r < lim ? st[kt][r] : -INFINITY;
   }
-  // row max: two v_max3 per key tile
+  // row max: four independent v_max3 chains (one per accumulator element) instead of one 26-deep
+  // dependent chain; the same instruction count
   float mx;
-#ifdef VCAP_ATTN_SERIAL_MAX
-  mx = -INFINITY;
-#pragma unroll
-  for (int kt = 0; kt < KE; ++kt) mx = max3f(max3f(mx, st[kt][0], st[kt][1]), st[kt][2], st[kt][3]);
-#else
   {
-    // four independent v_max3 chains (one per accumulator element) instead of one 26-deep
-    // dependent chain; the same instruction count
     float m4[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -247,35 +234,7 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
     }
     mx = fmaxf(max3f(m4[0], m4[1], m4[2]), m4[3]);
   }
-#endif
   mx = rows_max(mx);
-#ifdef VCAP_ATTN_PACKED_SOFTMAX
-  const f32x2 c2v = (f32x2){c2, c2}, nmx = (f32x2){-mx * c2, -mx * c2};
-  f32x2 sum2 = (f32x2){0.f, 0.f};
-#pragma unroll
-  for (int kt = 0; kt < KE; ++kt)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x2 a = pk_fma((f32x2){st[kt][2 * h], st[kt][2 * h + 1]}, c2v, nmx);
-      const f32x2 p = (f32x2){__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
-      st[kt][2 * h] = p.x;
-      st[kt][2 * h + 1] = p.y;
-      sum2 += p;
-    }
-  const float sum = rows_sum(sum2.x + sum2.y);
-#elif defined(VCAP_ATTN_VALU_SUM)
-  const float mxc = mx * c2;
-  float sum = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < KE; ++kt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float p = __builtin_amdgcn_exp2f(fmaf(st[kt][r], c2, -mxc));
-      st[kt][r] = p;
-      sum += p;
-    }
-  sum = rows_sum(sum);
-#else
   // the row sum comes out of the PV MFMAs below (a ones operand beside V), so the softmax here
   // is one FMA + one exp per score
   const float mxc = mx * c2;
@@ -283,18 +242,15 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
   for (int kt = 0; kt < KE; ++kt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], c2, -mxc));
-#endif
 
   // O^T[d][q] = sum_key V[key][d] P^T[key][q]; k element j of lane group g <-> key
   // 32c + 4g + j (j < 4) / 32c + 16 + 4g + (j - 4), matching the P^T fragment below
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#if !defined(VCAP_ATTN_VALU_SUM) && !defined(VCAP_ATTN_PACKED_SOFTMAX)
   // S[q] = sum_key 1 * P^T[key][q]: every output row of this MFMA is the sum of the bf16 P the
   // PV products use (lane (fr, fg) gets query fr's sum in each element)
   f32x4 osum = (f32x4){0.f, 0.f, 0.f, 0.f};
   const u32x4 ones = (u32x4){0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
-#endif
   const int qr = fr >> 2, p4 = fr & 3;
 #pragma unroll
   for (int c = 0; c < KT / 2; ++c) {
@@ -311,19 +267,15 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
                                                     : tr_read(Vs + r1 * 128 + ((ch ^ (r1 & 7)) << 4) + 8 * (p4 & 1));
       o[dt] = mfma_frag((u32x4){lo.x, lo.y, hi.x, hi.y}, pf, o[dt], (bf16_t*)nullptr);
     }
-#if !defined(VCAP_ATTN_VALU_SUM) && !defined(VCAP_ATTN_PACKED_SOFTMAX)
     osum = mfma_frag(ones, pf, osum, (bf16_t*)nullptr);
-#endif
   }
-#if !defined(VCAP_ATTN_VALU_SUM) && !defined(VCAP_ATTN_PACKED_SOFTMAX)
   const float sum = osum[0];
-#endif
   inv = __builtin_amdgcn_rcpf(sum);
 }
 
 // A query tile's output, packed for its stores: bf16 -> two dwordx4 per lane (lane pair exchange),
 // MXFP8 -> one dwordx4 per lane + the lane group 0 scale bytes.  Built right after the compute;
-// `attn_commit` stores it (the pipelined kernel defers that past its next loads).
+// `attn_commit` stores it.
 struct AttnOut {
   u32x4 w0, w1;
   int sb0, sb1;
@@ -397,12 +349,12 @@ VCAP_DEV void attn_commit(const AttnOut& r, void* out, int D, int h, uint8_t* os
 }
 
 // One workgroup per (frame, head) pair; two of them share a CU (56 KiB of LDS, <= 128 VGPRs
-// for 4 waves per SIMD), so one pair's DMA overlaps the other's MFMA / softmax.  Used for the
-// CLS-only last block, the L/14 shapes and (VCAP_ATTN_PIPE=0) everywhere.
+// for 4 waves per SIMD), so one pair's DMA overlaps the other's MFMA / softmax.  (A persistent
+// double-buffered walk over pairs measured equal alone and slower in the bench, r02: removed.)
 // MXO: write the output as MXFP8 (e4m3 + E8M0 per 32 of the head's 64 dims) for an MXFP8 attn-proj
 // GEMM; oscale in the vcap_common.h layout over `groups` 256-row groups.
 template <int KT, int KE, int WAVES, bool MXO>
-__global__ __launch_bounds__(WAVES * 64, KT == 14 ? VCAP_ATTN_WAVES_PER_SIMD : 1) void vcap_vit_attention_bf16_kernel(const bf16_t* __restrict__ qkv,
+__global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(const bf16_t* __restrict__ qkv,
                                                                              void* __restrict__ out, int N, int H,
                                                                              uint8_t* __restrict__ oscale,
                                                                              int groups, int cls_only) {
@@ -424,7 +376,6 @@ __global__ __launch_bounds__(WAVES * 64, KT == 14 ? VCAP_ATTN_WAVES_PER_SIMD : 1
   const int fr = lane & 15, fg = lane >> 4;
 
   // ---- K, V -> LDS by DMA (rows past N re-read row N-1: finite, masked out of the softmax)
-#ifndef VCAP_DIAG_ATTN_NOLOAD
   for (int blk = wave; blk < NS / 8; blk += WAVES) {
     const int r = blk * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (r & 7);
@@ -432,7 +383,6 @@ __global__ __launch_bounds__(WAVES * 64, KT == 14 ? VCAP_ATTN_WAVES_PER_SIMD : 1
     glds16_attn(src + D, Ks + blk * 1024);
     glds16_attn(src + 2 * D, Vs + blk * 1024);
   }
-#endif
   (void)NP;
   // ---- this wave's Q fragments
   const int qtiles = cls_only ? 1 : (N + 15) / 16;
@@ -452,127 +402,12 @@ __global__ __launch_bounds__(WAVES * 64, KT == 14 ? VCAP_ATTN_WAVES_PER_SIMD : 1
     if (qt >= qtiles) break;
     f32x4 o[4];
     float inv;
-#ifdef VCAP_DIAG_ATTN_NOCOMP
-    for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    inv = 1.f;
-#else
     attn_bf16_qtile<KT, KE>(Ks, Vs, qf[i], N, o, inv);
-#endif
     const int q = qt * 16 + fr;
     const bool keep = q < N && (!cls_only || q == 0);
     const long row = cls_only ? (long)bt : (long)bt * N + q;
     attn_commit<MXO>(attn_pack<MXO>(o, inv, row, keep), out, D, h, oscale, groups);
   }
-}
-
-// Pipelined variant for the full-sequence blocks: one workgroup per CU walks (frame, head) items
-// blockIdx.x, + gridDim.x, ...  K / V images are double-buffered and Q is staged in LDS too, so
-// while the waves compute item i the DMA of item i + 1 is in flight, and item i - 1's output
-// stores are issued right after that DMA (the vector memory counter is in order, so stores issued
-// before the next wait would otherwise be waited on with the loads).  One query tile per wave.
-template <int KT, int KE, int WAVES, bool MXO>
-__global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_pipe_kernel(const bf16_t* __restrict__ qkv,
-                                                                             void* __restrict__ out, int N, int H,
-                                                                             int items, uint8_t* __restrict__ oscale,
-                                                                             int groups) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NP = KT * 16;
-  constexpr int QP = (KT - 1) * 16;  // staged query rows (N > NP - 16 -> (N + 15) / 16 == KT - 1 tiles)
-  static_assert(KT % 2 == 0 && KT - 1 <= WAVES, "one query tile per wave");
-  char* Q = smem + 4 * NP * 128;
-  const int D = H * 64;
-  const long ld = 3L * D;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15, fg = lane >> 4;
-  const int qtiles = (N + 15) / 16;
-
-  auto issue = [&](int item, int buf) {
-#ifdef VCAP_DIAG_ATTN_NOLOAD
-    return;
-#endif
-    const int bt = item / H, h = item - bt * H;
-    const bf16_t* base = qkv + (long)bt * N * ld + h * 64;
-    char* Ks = smem + buf * 2 * NP * 128;
-    char* Vs = Ks + NP * 128;
-    for (int blk = wave; blk < NP / 8; blk += WAVES) {
-      const int r = blk * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ (r & 7);
-      const bf16_t* src = base + (long)min(r, N - 1) * ld + c * 8;
-      glds16_attn(src + D, Ks + blk * 1024);
-      glds16_attn(src + 2 * D, Vs + blk * 1024);
-    }
-    for (int blk = wave; blk < QP / 8; blk += WAVES) {
-      const int r = blk * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ (r & 7);
-      glds16_attn(base + (long)min(r, N - 1) * ld + c * 8, Q + blk * 1024);
-    }
-  };
-
-  int item = blockIdx.x, buf = 0;
-  if (item < items) issue(item, 0);
-  AttnOut pend;
-  pend.keep = false;
-  int pend_h = 0;
-  for (; item < items; item += gridDim.x, buf ^= 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // item's K / V / Q landed for every wave
-    const int qt = wave;
-    const int qrow = qt * 16 + fr;
-    u32x4 qf[2] = {(u32x4){0u, 0u, 0u, 0u}, (u32x4){0u, 0u, 0u, 0u}};
-    if (qt < qtiles) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        qf[s] = *reinterpret_cast<const u32x4*>(Q + qrow * 128 + (((s * 4 + fg) ^ (qrow & 7)) << 4));
-    }
-    __syncthreads();  // Q image free for the next item
-    const int next = item + gridDim.x;
-    if (next < items) issue(next, buf ^ 1);
-    attn_commit<MXO>(pend, out, D, pend_h, oscale, groups);
-    pend.keep = false;
-    if (qt < qtiles) {
-      const char* Ks = smem + buf * 2 * NP * 128;
-      f32x4 o[4];
-      float inv;
-#ifdef VCAP_DIAG_ATTN_NOCOMP
-      for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      inv = 1.f;
-#else
-      attn_bf16_qtile<KT, KE>(Ks, Ks + NP * 128, qf, N, o, inv);
-#endif
-      const int bt = item / H;
-      pend = attn_pack<MXO>(o, inv, (long)bt * N + qrow, qrow < N);
-      pend_h = item - bt * H;
-    }
-  }
-  attn_commit<MXO>(pend, out, D, pend_h, oscale, groups);
-}
-
-template <int KT, int KE, int WAVES, bool MXO>
-static hipError_t launch_attn_pipe(const void* qkv, void* out, int BT, int N, int H, uint8_t* oscale,
-                                   hipStream_t s) {
-  const size_t lds = (size_t)4 * KT * 16 * 128 + (size_t)(KT - 1) * 16 * 128;
-  static bool configured = false;
-  if (!configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_pipe_kernel<KT, KE, WAVES, MXO>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    configured = true;
-  }
-  const int items = BT * H;
-  const int groups = (BT * N + 255) / 256;
-  const int grid = std::min(items, vcap_device_cus());
-  hipLaunchKernelGGL((vcap_vit_attention_pipe_kernel<KT, KE, WAVES, MXO>), dim3(grid), dim3(WAVES * 64), lds, s,
-                     (const bf16_t*)qkv, out, N, H, items, oscale, groups);
-  return hipGetLastError();
-}
-
-static bool attn_pipe_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("VCAP_ATTN_PIPE");
-    return e && e[0] == '1';
-  }();
-  return on;
 }
 
 template <int KT, int KE, int WAVES, bool MXO>
@@ -609,8 +444,7 @@ static hipError_t launch_attn(const void* qkv, void* out, int BT, int N, int H, 
   return hipGetLastError();
 }
 
-// bf16 kernel choice: the pipelined walk for the full-sequence ViT-B/16 blocks (13 query tiles),
-// the per-(frame, head) kernel otherwise; KE = key tiles that can hold real keys
+// bf16 kernel choice by padded key count; KE = key tiles that can hold real keys
 template <bool MXO>
 static hipError_t attn_bf16_dispatch(const void* qkv, void* out, uint8_t* oscale, int BT, int N, int H,
                                      int cls_only, hipStream_t s) {
@@ -618,8 +452,6 @@ static hipError_t attn_bf16_dispatch(const void* qkv, void* out, uint8_t* oscale
     case 2: return launch_attn_bf16<2, 2, 4, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
     case 14:
       if (N <= 13 * 16) {
-        if (!cls_only && N > 12 * 16 && attn_pipe_enabled())
-          return launch_attn_pipe<14, 13, 16, MXO>(qkv, out, BT, N, H, oscale, s);
         return launch_attn_bf16<14, 13, 8, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
       }
       return launch_attn_bf16<14, 14, 8, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);

@@ -19,8 +19,10 @@ def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def gather_ids(local: torch.Tensor, world: int, group=None) -> torch.Tensor:
-    """[B_local, L] int32 per rank -> [world * B_local, L] on every rank (equal B_local per rank)."""
-    if world == 1:
+    """[B_local, L] int32 per rank -> [world * B_local, L] on every rank (equal B_local per rank).
+    A single process without a process group returns `local`; an initialised group of one rank
+    still runs the collective (the RCCL path of a one-GPU job)."""
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return local
     if dist.get_backend(group) == "nccl":
         out = torch.empty(world * local.shape[0], *local.shape[1:], dtype=local.dtype, device=local.device)

@@ -10,7 +10,8 @@ for f in $(git -C $root ls-tree --name-only $rev video-caption-algorithm_amd/csr
 git -C $root show $rev:include/vcap.h > $d/include/vcap.h
 mkdir -p $d/../include && cp $d/include/vcap.h $d/../include/vcap.h   # runtime.hip includes ../../include/vcap.h
 for f in $d/csrc/*.hip; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -Wno-unused-result \
+  extra=""; [ "$(basename $f)" = vit_attention.hip ] && extra="-fno-honor-nans"   # as vcap/build.py FILE_FLAGS
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -Wno-unused-result $extra \
     -I$d/csrc -I$d/include -c $f -o $d/obj/$(basename $f .hip).o &
 done
 wait

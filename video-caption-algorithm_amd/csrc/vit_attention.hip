@@ -193,13 +193,11 @@ VCAP_DEV u32x2 tr_read(const char* p) {
 // KE: key tiles that can hold real keys (KT or KT - 1: with N <= 16 (KT - 1) the last tile is all
 // padding, kept only as the zero half of the last 32-key PV chunk - no S, max or exp for it).
 template <int KT, int KE>
-VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[2], int N, f32x4 (&o)[4],
-                              float& inv) {
+VCAP_DEV void attn_qk_softmax(const char* Ks, const u32x4 (&qf)[2], int N, f32x4 (&st)[KT]) {
   const int lane = threadIdx.x & 63;
   const int fr = lane & 15, fg = lane >> 4;
   const float c2 = 0.125f * 1.4426950408889634f;  // 64^-0.5 * log2(e)
   // S^T[key][q] = K . Q^T
-  f32x4 st[KT];
   if constexpr (KE < KT) st[KT - 1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int kt = 0; kt < KE; ++kt) {
@@ -242,7 +240,13 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
   for (int kt = 0; kt < KE; ++kt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], c2, -mxc));
+}
 
+// O^T = V^T.P^T of a tile whose exp'd scores st came from attn_qk_softmax
+template <int KT, int KE>
+VCAP_DEV void attn_pv(const char* Vs, const f32x4 (&st)[KT], f32x4 (&o)[4], float& inv) {
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, fg = lane >> 4;
   // O^T[d][q] = sum_key V[key][d] P^T[key][q]; k element j of lane group g <-> key
   // 32c + 4g + j (j < 4) / 32c + 16 + 4g + (j - 4), matching the P^T fragment below
 #pragma unroll
@@ -271,6 +275,20 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
   }
   const float sum = osum[0];
   inv = __builtin_amdgcn_rcpf(sum);
+}
+
+template <int KT, int KE>
+VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[2], int N, f32x4 (&o)[4],
+                              float& inv) {
+  f32x4 st[KT];
+  attn_qk_softmax<KT, KE>(Ks, qf, N, st);
+  attn_pv<KT, KE>(Vs, st, o, inv);
+}
+
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their maxima; gfx9 field layout)
+template <int N>
+VCAP_DEV void wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
 // A query tile's output, packed for its stores: bf16 -> two dwordx4 per lane (lane pair exchange),
@@ -375,16 +393,22 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
 
-  // ---- K, V -> LDS by DMA (rows past N re-read row N-1: finite, masked out of the softmax)
-  for (int blk = wave; blk < NS / 8; blk += WAVES) {
-    const int r = blk * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ (r & 7);
-    const bf16_t* src = base + (long)min(r, N - 1) * ld + c * 8;
-    glds16_attn(src + D, Ks + blk * 1024);
-    glds16_attn(src + 2 * D, Vs + blk * 1024);
-  }
+  // ---- K -> LDS by DMA, then this wave's Q fragments, then V -> LDS (rows past N re-read row N-1:
+  // finite, masked out of the softmax).  Every wave issues the same number of DMA pieces (the
+  // excess ones re-write the last block with identical bytes), so the waits below are immediates:
+  // the first query tile's S = K.Q^T and softmax run while the V rows are still landing.
+  constexpr int NB = NS / 8, PER = (NB + WAVES - 1) / WAVES;
+  auto dma = [&](int off, char* img) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int blk = min(wave + i * WAVES, NB - 1);
+      const int r = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      glds16_attn(base + (long)min(r, N - 1) * ld + c * 8 + off, img + blk * 1024);
+    }
+  };
+  dma(D, Ks);
   (void)NP;
-  // ---- this wave's Q fragments
   const int qtiles = cls_only ? 1 : (N + 15) / 16;
   u32x4 qf[QT_MAX][2];
 #pragma unroll
@@ -393,11 +417,29 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
 #pragma unroll
     for (int s = 0; s < 2; ++s) qf[i][s] = *reinterpret_cast<const u32x4*>(base + (long)q * ld + s * 32 + fg * 8);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  dma(2 * D, Vs);
+  wait_vmcnt<PER>();  // this wave's K pieces and Q landed (its V pieces may not have)
+  __syncthreads();    // every wave's K pieces landed
 
+  // first query tile: S and softmax before the V wait
+  {
+    const int qt = wave;
+    f32x4 st[KT];
+    if (qt < qtiles) attn_qk_softmax<KT, KE>(Ks, qf[0], N, st);
+    wait_vmcnt<0>();
+    __syncthreads();  // every wave's V pieces landed
+    if (qt < qtiles) {
+      f32x4 o[4];
+      float inv;
+      attn_pv<KT, KE>(Vs, st, o, inv);
+      const int q = qt * 16 + fr;
+      const bool keep = q < N && (!cls_only || q == 0);
+      const long row = cls_only ? (long)bt : (long)bt * N + q;
+      attn_commit<MXO>(attn_pack<MXO>(o, inv, row, keep), out, D, h, oscale, groups);
+    }
+  }
 #pragma unroll
-  for (int i = 0; i < QT_MAX; ++i) {
+  for (int i = 1; i < QT_MAX; ++i) {
     const int qt = wave + i * WAVES;
     if (qt >= qtiles) break;
     f32x4 o[4];

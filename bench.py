@@ -76,8 +76,6 @@ def parse():
                     help="consecutive batches encoded together as one encode (divides --dec-group); 0 = auto: "
                          "2 while a batch holds <= 128 frames (the N = 768 GEMMs of one 8 x 16-frame batch fill "
                          "1.16 rounds of 256 tiles), else 1")
-    ap.add_argument("--decode-priority", default="high", choices=["high", "normal"],
-                    help="stream priority of the decode lanes (the encode stream is normal)")
     ap.add_argument("--confine-decode", action="store_true",
                     help="mask the decode streams to the reserved CUs (default: unmasked, high priority)")
     ap.add_argument("--gemm-policy", type=int, default=0, help="vcap_set_gemm_policy value for A/B runs (0 = auto)")
@@ -330,7 +328,6 @@ def main():
                            reserve_cus=0 if args.serial else args.reserve_cus,
                            dec_lanes=1 if args.serial else args.dec_lanes,
                            confine_decode=args.confine_decode and not args.serial,
-                           decode_priority=args.decode_priority,
                            dec_group=1 if args.serial else args.dec_group,
                            enc_group=1 if args.serial else args.enc_group)
 

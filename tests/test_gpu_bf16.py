@@ -23,7 +23,7 @@ from vcap.model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, trim
 pytestmark = pytest.mark.gpu
 
 BF16_LOGIT_TOL = 0.02          # |bf16 HIP - fp32 reference| on every raw logit the golden records (measured max 0.013)
-FREE_RUN_PREFIX_FLOOR = 0.9    # mean fraction of each caption's leading tokens equal to the reference's (measured 1.0)
+BF16_E2E_TOL = 0.03            # the same bound for bf16 encoder + decoder (tests/test_gpu_fidelity.py, measured 0.019)
 _CACHE = {}
 
 
@@ -117,11 +117,23 @@ def token_agreement(got, ref):
 
 def test_bf16_free_running_agreement(device):
     """The benchmark's bf16 path end to end (encode + fused greedy decode graph) against the
-    reference's HF-greedy captions of the same 8 videos."""
+    reference's HF-greedy captions of the same 8 videos.  The floor is argued, not measured: with
+    every processed score within BF16_E2E_TOL of the reference's, no token can differ before the
+    first step whose reference processed top-2 gap is <= 2 x BF16_E2E_TOL (gaps from the golden
+    all-step logits); each caption's leading agreement must reach that step, and every divergence
+    must start at such a near-tie."""
+    meta, g, va, ga, sd, frames, enc, pre, dec = _models("bf16", device)
     got, ref = _free_running(device)
+    B, L, eos = ref.shape[0], ref.shape[1], ga.eos_token_id
+    gaps = np.stack([_processed_top2_gap(*_golden_step(g, s), ref[:, :s], ga.vocab, eos, s)[0] for s in range(L)], 1)
     lead, pos = token_agreement(got, ref)
+    for b in range(B):
+        first_div = next((s for s in range(L) if got[b, s] != ref[b, s]), L)
+        guard = next((s for s in range(L) if gaps[b, s] <= 2 * BF16_E2E_TOL), L)
+        assert first_div >= guard, (b, first_div, guard, gaps[b, :first_div + 1])
+        if first_div < L:
+            assert gaps[b, first_div] <= 2 * BF16_E2E_TOL, (b, first_div, gaps[b, first_div])
     print(f"bf16 free-running: leading-token agreement {lead:.3f}, position-wise {pos:.3f}")
-    assert lead >= FREE_RUN_PREFIX_FLOOR, (lead, got, ref)
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp32"])

@@ -187,26 +187,6 @@ def test_attention_mx_output(device, tokens, heads):
     assert (np.abs(got - r) <= half_step + np.abs(r) * 2.0 ** -8 + 1e-12).all()
 
 
-FP8_LEAD_FLOOR = 0.25  # mean leading-token agreement of fp8-encoder captions with the reference's (measured 0.33)
-
-
-def test_fp8_caption_token_agreement(device):
-    """Caption-level fidelity of the MXFP8 encoder (configs[4]): encode the b16_b8 clips with fp8
-    ViT GEMMs, decode with the bf16 greedy graph, and compare the HF-greedy captions with the
-    reference's (tests/golden/b16_b8) - leading-token agreement above a stated floor (fp8 operand
-    rounding moves the prefix; near-tied greedy choices then legitimately diverge)."""
-    from vcap.model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder
-    meta, g, va, ga, sd, frames = case("b16_b8")
-    enc = HipViTEncoder(sd, va, "fp8", device)
-    dec = HipGPT2Decoder(sd, ga, "bf16", device)
-    _, prefix = enc.encode(torch.from_numpy(frames).to(device), HipPrefix(sd, ga.n_embd, device=device))
-    ids = dec.generate_ids(prefix, [ga.bos_token_id], GenConfig(24, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id))
-    got, ref = ids.cpu().numpy(), g["hf_greedy_ids"]
-    lead = []
-    for a, b in zip(got, ref):
-        n = 0
-        while n < len(b) and a[n] == b[n]:
-            n += 1
-        lead.append(n / len(b))
-    print(f"fp8 captions: leading-token agreement {np.mean(lead):.3f}, position-wise {(got == ref).mean():.3f}")
-    assert np.mean(lead) >= FP8_LEAD_FLOOR, (lead, got, ref)
+# Caption-level fidelity of the MXFP8 encoder (configs[4]): tests/test_gpu_fidelity.py
+# (test_fp8_divergences_are_near_ties: every divergence explained by an fp32 near-tie, leading-token
+# agreement at least the floor the margins guarantee; the r02 measured floor is retired).

@@ -193,11 +193,13 @@ VCAP_DEV u32x2 tr_read(const char* p) {
 // KE: key tiles that can hold real keys (KT or KT - 1: with N <= 16 (KT - 1) the last tile is all
 // padding, kept only as the zero half of the last 32-key PV chunk - no S, max or exp for it).
 template <int KT, int KE>
-VCAP_DEV void attn_qk_softmax(const char* Ks, const u32x4 (&qf)[2], int N, f32x4 (&st)[KT]) {
+VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[2], int N, f32x4 (&o)[4],
+                              float& inv) {
   const int lane = threadIdx.x & 63;
   const int fr = lane & 15, fg = lane >> 4;
   const float c2 = 0.125f * 1.4426950408889634f;  // 64^-0.5 * log2(e)
   // S^T[key][q] = K . Q^T
+  f32x4 st[KT];
   if constexpr (KE < KT) st[KT - 1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int kt = 0; kt < KE; ++kt) {
@@ -240,13 +242,7 @@ VCAP_DEV void attn_qk_softmax(const char* Ks, const u32x4 (&qf)[2], int N, f32x4
   for (int kt = 0; kt < KE; ++kt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) st[kt][r] = __builtin_amdgcn_exp2f(fmaf(st[kt][r], c2, -mxc));
-}
 
-// O^T = V^T.P^T of a tile whose exp'd scores st came from attn_qk_softmax
-template <int KT, int KE>
-VCAP_DEV void attn_pv(const char* Vs, const f32x4 (&st)[KT], f32x4 (&o)[4], float& inv) {
-  const int lane = threadIdx.x & 63;
-  const int fr = lane & 15, fg = lane >> 4;
   // O^T[d][q] = sum_key V[key][d] P^T[key][q]; k element j of lane group g <-> key
   // 32c + 4g + j (j < 4) / 32c + 16 + 4g + (j - 4), matching the P^T fragment below
 #pragma unroll
@@ -275,20 +271,6 @@ VCAP_DEV void attn_pv(const char* Vs, const f32x4 (&st)[KT], f32x4 (&o)[4], floa
   }
   const float sum = osum[0];
   inv = __builtin_amdgcn_rcpf(sum);
-}
-
-template <int KT, int KE>
-VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[2], int N, f32x4 (&o)[4],
-                              float& inv) {
-  f32x4 st[KT];
-  attn_qk_softmax<KT, KE>(Ks, qf, N, st);
-  attn_pv<KT, KE>(Vs, st, o, inv);
-}
-
-// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their maxima; gfx9 field layout)
-template <int N>
-VCAP_DEV void wait_vmcnt() {
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
 // A query tile's output, packed for its stores: bf16 -> two dwordx4 per lane (lane pair exchange),
@@ -368,7 +350,9 @@ VCAP_DEV void attn_commit(const AttnOut& r, void* out, int D, int h, uint8_t* os
 
 // One workgroup per (frame, head) pair; two of them share a CU (56 KiB of LDS, <= 128 VGPRs
 // for 4 waves per SIMD), so one pair's DMA overlaps the other's MFMA / softmax.  (A persistent
-// double-buffered walk over pairs measured equal alone and slower in the bench, r02: removed.)
+// double-buffered walk over pairs measured equal alone and slower in the bench, r02: removed.
+// Issuing K, Q, then V and running the first query tile's S + softmax before the V wait measured
+// 39.1-39.7 vs 37.8-38.6 us at 128 frames, r03 (profiles/r03_attention_v_overlap_ab.txt): reverted.)
 // MXO: write the output as MXFP8 (e4m3 + E8M0 per 32 of the head's 64 dims) for an MXFP8 attn-proj
 // GEMM; oscale in the vcap_common.h layout over `groups` 256-row groups.
 template <int KT, int KE, int WAVES, bool MXO>
@@ -393,22 +377,16 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
 
-  // ---- K -> LDS by DMA, then this wave's Q fragments, then V -> LDS (rows past N re-read row N-1:
-  // finite, masked out of the softmax).  Every wave issues the same number of DMA pieces (the
-  // excess ones re-write the last block with identical bytes), so the waits below are immediates:
-  // the first query tile's S = K.Q^T and softmax run while the V rows are still landing.
-  constexpr int NB = NS / 8, PER = (NB + WAVES - 1) / WAVES;
-  auto dma = [&](int off, char* img) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int blk = min(wave + i * WAVES, NB - 1);
-      const int r = blk * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ (r & 7);
-      glds16_attn(base + (long)min(r, N - 1) * ld + c * 8 + off, img + blk * 1024);
-    }
-  };
-  dma(D, Ks);
+  // ---- K, V -> LDS by DMA (rows past N re-read row N-1: finite, masked out of the softmax)
+  for (int blk = wave; blk < NS / 8; blk += WAVES) {
+    const int r = blk * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    const bf16_t* src = base + (long)min(r, N - 1) * ld + c * 8;
+    glds16_attn(src + D, Ks + blk * 1024);
+    glds16_attn(src + 2 * D, Vs + blk * 1024);
+  }
   (void)NP;
+  // ---- this wave's Q fragments
   const int qtiles = cls_only ? 1 : (N + 15) / 16;
   u32x4 qf[QT_MAX][2];
 #pragma unroll
@@ -417,29 +395,11 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
 #pragma unroll
     for (int s = 0; s < 2; ++s) qf[i][s] = *reinterpret_cast<const u32x4*>(base + (long)q * ld + s * 32 + fg * 8);
   }
-  dma(2 * D, Vs);
-  wait_vmcnt<PER>();  // this wave's K pieces and Q landed (its V pieces may not have)
-  __syncthreads();    // every wave's K pieces landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
-  // first query tile: S and softmax before the V wait
-  {
-    const int qt = wave;
-    f32x4 st[KT];
-    if (qt < qtiles) attn_qk_softmax<KT, KE>(Ks, qf[0], N, st);
-    wait_vmcnt<0>();
-    __syncthreads();  // every wave's V pieces landed
-    if (qt < qtiles) {
-      f32x4 o[4];
-      float inv;
-      attn_pv<KT, KE>(Vs, st, o, inv);
-      const int q = qt * 16 + fr;
-      const bool keep = q < N && (!cls_only || q == 0);
-      const long row = cls_only ? (long)bt : (long)bt * N + q;
-      attn_commit<MXO>(attn_pack<MXO>(o, inv, row, keep), out, D, h, oscale, groups);
-    }
-  }
 #pragma unroll
-  for (int i = 1; i < QT_MAX; ++i) {
+  for (int i = 0; i < QT_MAX; ++i) {
     const int qt = wave + i * WAVES;
     if (qt >= qtiles) break;
     f32x4 o[4];

@@ -42,7 +42,7 @@ class CaptionPipeline:
     def __init__(self, encoder: HipViTEncoder, prefix: HipPrefix, decoder: HipGPT2Decoder, cfg: GenConfig,
                  batch: int, prompt_ids: Sequence[int], device, depth: int = 2, gather=None,
                  reserve_cus: int = 0, dec_lanes: int = 1, confine_decode: bool = False, dec_group: int = 1,
-                 enc_group: int = 1, decode_priority: str = "high"):
+                 enc_group: int = 1):
         self.enc, self.pre, self.dec, self.cfg = encoder, prefix, decoder, cfg
         self.prompt_ids = list(prompt_ids)
         self.device = torch.device(device)
@@ -86,8 +86,8 @@ class CaptionPipeline:
                     self._dec_handles.append(h.value)
                 self.s_decs = [torch.cuda.ExternalStream(h, device=self.device) for h in self._dec_handles]
             else:
-                prio = {"high": hi, "normal": lo}[decode_priority]
-                self.s_decs = [torch.cuda.Stream(self.device, priority=prio) for _ in range(self.lanes)]
+                # (normal-priority decode lanes measured the same: 1224-1228 captions/s either way, r03)
+                self.s_decs = [torch.cuda.Stream(self.device, priority=hi) for _ in range(self.lanes)]
         self.s_dec = self.s_decs[0]
         # the encoder / decoder workspaces are shared with serial calls made on the creating stream:
         # nothing of the pipeline may start before that stream's pending work has finished

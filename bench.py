@@ -476,6 +476,9 @@ def main():
             "value_definition": "pipelined throughput: videos captioned / wall time of the timed steps "
                                 "(encodes overlapped with the decodes of earlier batches)",
             "captions_per_s_b_over_p50": world * B / (p50 / 1e3),
+            # the reference's own throughput definition (batch / mean iteration wall time,
+            # core/scripts/benchmark_baseline.py:291-292, 356-358) on the same per-batch latencies
+            "captions_per_s_b_over_mean": world * B / (statistics.mean(lat) / 1e3),
             "p50_latency_ms": p50,
             "new_tokens_per_caption": {"mean": sum(lens) / len(lens), "max": max(lens),
                                        "decode_steps_run": args.max_new},

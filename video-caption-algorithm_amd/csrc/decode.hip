@@ -701,7 +701,7 @@ __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // every load of the first phase issued at once (clamped addresses, selects after): the history,
   // the argmax partials (nblk <= 1024) and the row's finished flag
-  constexpr int HP = 4, PP = 4;
+  constexpr int HP = 4, PP = 8;
   int hv[HP], pi[PP];
   float pv[PP];
 #pragma unroll
@@ -834,7 +834,11 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
 // per token step, and forcing 3 workgroups per CU (<= 168 VGPRs) +22 us);
 // the projections take 1 unless a grid cap asks for wider workgroups (2 or 4 tiles).
 static int rows_ntb(int epi, int N = 0, int max_blocks = 0) {
-  if (epi == EPI_LOGITS || epi == EPI_LSE) return 4;
+#ifndef VCAP_LM_NTB
+#define VCAP_LM_NTB 4
+#endif
+  if (epi == EPI_LOGITS) return VCAP_LM_NTB;
+  if (epi == EPI_LSE) return 4;
   const int tiles = (N + 15) / 16;
   if (max_blocks <= 0 || tiles <= max_blocks) return 1;
   return tiles <= 2 * max_blocks ? 2 : 4;
@@ -865,7 +869,7 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
   if (pro == PRO_LN && epi == EPI_QKV) { VCAP_ROWS_NT(TT, PRO_LN, EPI_QKV) }                \
   if (pro == PRO_LN && epi == EPI_GELU) { VCAP_ROWS_NT(TT, PRO_LN, EPI_GELU) }              \
   if (pro == PRO_DIRECT && epi == EPI_RESID) { VCAP_ROWS_NT(TT, PRO_DIRECT, EPI_RESID) }    \
-  if (pro == PRO_LN && epi == EPI_LOGITS) { VCAP_ROWS(TT, PRO_LN, EPI_LOGITS, 4) }   \
+  if (pro == PRO_LN && epi == EPI_LOGITS) { VCAP_ROWS(TT, PRO_LN, EPI_LOGITS, VCAP_LM_NTB) }   \
   if (pro == PRO_LN && epi == EPI_LSE) { VCAP_ROWS(TT, PRO_LN, EPI_LSE, 4) }
   if (dt == VCAP_DT_BF16) {
     VCAP_ROWS_EPI(bf16_t)
@@ -1041,7 +1045,7 @@ hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const in
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,
                                          const float* wpe, float* h, int E, int pos_next, int vocab, hipStream_t s) {
-  if (hist_ld > 1024 || nblk < 1 || nblk > 1024 || step >= hist_ld) return hipErrorInvalidValue;
+  if (hist_ld > 1024 || nblk < 1 || nblk > 2048 || step >= hist_ld) return hipErrorInvalidValue;
   if (dt == VCAP_DT_BF16)
     hipLaunchKernelGGL((vcap_decode_finalize_kernel<bf16_t>), dim3(B), dim3(256), 0, s, part_val, part_idx, nblk,
                        step, finished, hist, hist_ld, banned, nbanned, ngram, eos, pad, out_ids, out_ld,

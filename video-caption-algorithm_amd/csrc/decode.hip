@@ -18,19 +18,28 @@
 // so every weight load is one fully coalesced 1 KiB wave instruction and a wave's whole K range
 // of a tile is one contiguous run (rows >= N are zero).
 #include "vcap_common.h"
-// Weight fragments: buffer loads (SGPR base = the kernel argument, one VGPR byte offset) with the
-// nontemporal policy.  nt keeps the decode's 247 MB per token step from evicting the concurrently
-// running encode's operand tiles (plain loads: encode stage +2 %, bench -2 %); the buffer form
-// instead of flat global loads cut the decode step 269.7 -> 263.5 us alone
-// (profiles/r02_decode_experiments.txt); the GEMV's activation / LayerNorm operands use the same
-// form with the default policy (263.4 -> 261.0 us).  Policy bits on gfx950: 1 = sc0, 2 = nt, 16 = sc1.
+// Weight fragments, nontemporal: nt keeps the decode's 247 MB per token step from evicting the
+// concurrently running encode's operand tiles (plain loads: encode stage +2 %, bench -2 %,
+// profiles/r02_decode_experiments.txt).  Two address forms, chosen per kernel by measurement
+// (profiles/r03_decode_load_form_ab.txt): flat global loads for the one-row-tile GEMV (MT = 1:
+// GPT-2-medium step 644 -> 564 us at 8 rows, beam 4 x 4 731 -> 651 us; GPT-2 small unchanged) and
+// buffer loads (SGPR base + one 32-bit VGPR offset) for the 32-row GEMV and the prefill kernel
+// (medium beam 8 x 4 930 vs 950 us flat, prefill 20-60 us faster).  Buffer-load policy bits on
+// gfx950: 1 = sc0, 2 = nt, 16 = sc1.
 template <int AUX = 0>
 __device__ __forceinline__ u32x4 vcap_buf_load16(const void* base, long off_bytes) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7FFFFFFF, 0x00020000);
   return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off_bytes, 0, AUX));
 }
+template <bool FLAT>
 __device__ __forceinline__ u32x4 vcap_dec_wload(const void* base, const void* p) {
-  return vcap_buf_load16<2>(base, (const char*)p - (const char*)base);
+  if constexpr (FLAT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  else return vcap_buf_load16<2>(base, (const char*)p - (const char*)base);
+}
+// The GEMV's activation / LayerNorm operands: buffer loads, default policy (flat: GPT-2 small
+// 260 -> 263 us per step).
+__device__ __forceinline__ u32x4 vcap_dec_aload(const void* base, long off_bytes) {
+  return vcap_buf_load16(base, off_bytes);
 }
 #include "vcap_kernels.h"
 
@@ -227,19 +236,19 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
     for (int i = 0; i < MT; ++i) {
       const long xo = (long)min(m0 + i * 16 + fr, M - 1) * a.ldx + fg * E;
 #pragma unroll
-      for (int s = 0; s < NSL; ++s) af[i][s] = vcap_buf_load16(a.x, (xo + (g0 + s) * KS) * (long)sizeof(T));
+      for (int s = 0; s < NSL; ++s) af[i][s] = vcap_dec_aload(a.x, (xo + (g0 + s) * KS) * (long)sizeof(T));
     }
   } else {
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
       const long xo = (long)min(m0 + wave + 4 * r, M - 1) * a.ldx + lane * 4;
 #pragma unroll
-      for (int c = 0; c < KC; ++c) xv[r][c] = __builtin_bit_cast(f32x4, vcap_buf_load16(a.x, (xo + c * 256) * 4L));
+      for (int c = 0; c < KC; ++c) xv[r][c] = __builtin_bit_cast(f32x4, vcap_dec_aload(a.x, (xo + c * 256) * 4L));
     }
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
-      gv[c] = __builtin_bit_cast(f32x4, vcap_buf_load16(a.ln_g, (c * 256 + lane * 4) * 4L));
-      bv[c] = __builtin_bit_cast(f32x4, vcap_buf_load16(a.ln_b, (c * 256 + lane * 4) * 4L));
+      gv[c] = __builtin_bit_cast(f32x4, vcap_dec_aload(a.ln_g, (c * 256 + lane * 4) * 4L));
+      bv[c] = __builtin_bit_cast(f32x4, vcap_dec_aload(a.ln_b, (c * 256 + lane * 4) * 4L));
     }
   }
 
@@ -251,7 +260,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   for (int j = 0; j < NTB; ++j) {
     const u32x4* wp = packed_frag(a.w, min(n0 / 16 + j, ntiles - 1), nslab, g0, lane);
 #pragma unroll
-    for (int s = 0; s < NSL; ++s) wf[s][j] = vcap_dec_wload(a.w, wp + s * 64);
+    for (int s = 0; s < NSL; ++s) wf[s][j] = vcap_dec_wload<MT == 1>(a.w, wp + s * 64);
   }
 
   // ---- 3) epilogue inputs
@@ -452,7 +461,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
       }
 #pragma unroll
       for (int j = 0; j < NTB; ++j)
-        wf[u][j] = vcap_dec_wload(a.w,
+        wf[u][j] = vcap_dec_wload<false>(a.w,
             packed_frag(a.w, min(n0 / 16 + j, ntiles - 1), nslab, g0 + sl, lane));
     }
   };
@@ -818,8 +827,11 @@ static bool try_gemv(int nsl, const RowsGemmArgs& a, hipStream_t s, hipError_t& 
 
 template <typename T, int MT, int NTB, int PRO, int EPI>
 static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
-  // the weight loads address the packed matrix with a 32-bit byte offset (vcap_dec_wload)
-  if ((long)(a.N + 63) * a.K * (long)sizeof(T) >= 0x7FFFFFFFL) return hipErrorInvalidValue;
+  // buffer loads address the packed weights (vcap_dec_wload<false>) and a.x (vcap_dec_aload; f32
+  // rows under PRO_LN) with 32-bit byte offsets
+  if ((long)(a.N + 63) * a.K * (long)sizeof(T) >= 0x7FFFFFFFL ||
+      (long)a.M * a.ldx * (long)(PRO == PRO_LN ? sizeof(float) : sizeof(T)) >= 0x7FFFFFFFL)
+    return hipErrorInvalidValue;
   const int nsl = a.K / (16 * Frag<T>::kElems);
   hipError_t err = hipSuccess;
   if (try_gemv<T, MT, NTB, PRO, EPI, 6>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 8>(nsl, a, s, err) ||
@@ -830,15 +842,11 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
 }
 
 // 16-column tiles per workgroup: the lm_head always takes 4 (argmax partials per 64 columns; 786
-// workgroups at 2 per CU.  r03: 5 or 8 tiles per workgroup (629 / 393 workgroups) measured +6 / +8 us
-// per token step, and forcing 3 workgroups per CU (<= 168 VGPRs) +22 us);
+// workgroups at 2 per CU.  r03: 2, 5 or 8 tiles per workgroup (1571 / 629 / 393 workgroups) measured
+// +1-2 / +6 / +8 us per token step, and forcing 3 workgroups per CU (<= 168 VGPRs) +22 us);
 // the projections take 1 unless a grid cap asks for wider workgroups (2 or 4 tiles).
 static int rows_ntb(int epi, int N = 0, int max_blocks = 0) {
-#ifndef VCAP_LM_NTB
-#define VCAP_LM_NTB 4
-#endif
-  if (epi == EPI_LOGITS) return VCAP_LM_NTB;
-  if (epi == EPI_LSE) return 4;
+  if (epi == EPI_LOGITS || epi == EPI_LSE) return 4;
   const int tiles = (N + 15) / 16;
   if (max_blocks <= 0 || tiles <= max_blocks) return 1;
   return tiles <= 2 * max_blocks ? 2 : 4;
@@ -869,7 +877,7 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
   if (pro == PRO_LN && epi == EPI_QKV) { VCAP_ROWS_NT(TT, PRO_LN, EPI_QKV) }                \
   if (pro == PRO_LN && epi == EPI_GELU) { VCAP_ROWS_NT(TT, PRO_LN, EPI_GELU) }              \
   if (pro == PRO_DIRECT && epi == EPI_RESID) { VCAP_ROWS_NT(TT, PRO_DIRECT, EPI_RESID) }    \
-  if (pro == PRO_LN && epi == EPI_LOGITS) { VCAP_ROWS(TT, PRO_LN, EPI_LOGITS, VCAP_LM_NTB) }   \
+  if (pro == PRO_LN && epi == EPI_LOGITS) { VCAP_ROWS(TT, PRO_LN, EPI_LOGITS, 4) }            \
   if (pro == PRO_LN && epi == EPI_LSE) { VCAP_ROWS(TT, PRO_LN, EPI_LSE, 4) }
   if (dt == VCAP_DT_BF16) {
     VCAP_ROWS_EPI(bf16_t)

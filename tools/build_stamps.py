@@ -1,0 +1,103 @@
+"""Diagnostic build of libvcap_hip.so whose decode kernels stamp the 100 MHz real-time clock
+(s_memrealtime) at fixed points: workgroup entry, activation operand ready (after the LayerNorm /
+A-fragment barrier), MFMAs retired (split-K partials written), reduction barrier passed, epilogue
+issued.  The product sources are not touched: this script patches a copy under /tmp and builds
+video-caption-algorithm_amd/vcap/_lib/libvcap_stamps.so (use it with VCAP_LIB=..., read with
+tools/decode_stamps.py).  Stamps go to a __device__ buffer that nothing else reads.
+"""
+import os
+import re
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+SRC = ROOT / "video-caption-algorithm_amd" / "csrc"
+OUT = ROOT / "video-caption-algorithm_amd" / "vcap" / "_lib" / "libvcap_stamps.so"
+
+HEADER = r'''
+__device__ unsigned long long g_vcap_stamps[8 << 18];
+__device__ unsigned int g_vcap_stamp_n;
+#define VCAP_RT() ({ asm volatile("" ::: "memory"); unsigned long long _t = __builtin_amdgcn_s_memrealtime(); asm volatile("" ::: "memory"); _t; })
+__device__ __forceinline__ void vcap_stamp_rec(unsigned long long tag, unsigned long long t0, unsigned long long t1,
+                                               unsigned long long t2, unsigned long long t3, unsigned long long t4) {
+  const unsigned i = atomicAdd(&g_vcap_stamp_n, 1u);
+  if (i < (1u << 18)) {
+    unsigned long long* r = g_vcap_stamps + 8ull * i;
+    r[0] = tag; r[1] = blockIdx.x | ((unsigned long long)gridDim.x << 20) | ((unsigned long long)blockIdx.y << 40);
+    r[2] = t0; r[3] = t1; r[4] = t2; r[5] = t3; r[6] = t4; r[7] = 0;
+  }
+}
+extern "C" __attribute__((visibility("default"))) int vcap_diag_stamps(void* host, int max_rec) {
+  unsigned n = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_vcap_stamp_n), sizeof(n)) != hipSuccess) return -1;
+  if (n > (1u << 18)) n = 1u << 18;
+  if (host && max_rec > 0) {
+    const unsigned k = n < (unsigned)max_rec ? n : (unsigned)max_rec;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_vcap_stamps), 64ull * k) != hipSuccess) return -1;
+  }
+  const unsigned z = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_vcap_stamp_n), &z, sizeof(z)) != hipSuccess) return -1;
+  return (int)n;
+}
+'''
+
+
+def patch_decode(s: str) -> str:
+    s = s.replace('#include "vcap_kernels.h"\n', '#include "vcap_kernels.h"\n' + HEADER, 1)
+    # GEMV kernel
+    k0 = s.index("__global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {")
+    k1 = s.index("// General rows kernel", k0)
+    body = s[k0:k1]
+    body = body.replace("  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n",
+                        "  const unsigned long long t0 = VCAP_RT();\n  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n", 1)
+    body = body.replace("  if constexpr (PRO == PRO_LN || EPI == EPI_LOGITS) __syncthreads();\n",
+                        "  if constexpr (PRO == PRO_LN || EPI == EPI_LOGITS) __syncthreads();\n  const unsigned long long t1 = VCAP_RT();\n", 1)
+    body = body.replace("  if constexpr (EPI == EPI_LOGITS) toks.template mark<NTB>(a, m0, n0, s_rep, s_ban);\n  __syncthreads();\n",
+                        "  const unsigned long long t2 = VCAP_RT();\n  if constexpr (EPI == EPI_LOGITS) toks.template mark<NTB>(a, m0, n0, s_rep, s_ban);\n  __syncthreads();\n  const unsigned long long t3 = VCAP_RT();\n", 1)
+    body = body.replace("  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0);\n}",
+                        "  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0);\n"
+                        "  if (threadIdx.x == 0) vcap_stamp_rec((unsigned long long)((NSL << 12) | (EPI << 8) | (PRO << 4) | NTB) | ((unsigned long long)MT << 20), t0, t1, t2, t3, VCAP_RT());\n}", 1)
+    assert body.count("VCAP_RT()") == 5, body.count("VCAP_RT()")
+    s = s[:k0] + body + s[k1:]
+    # decode attention (c64)
+    a0 = s.index("void vcap_decode_attention_c64_kernel(")
+    a1 = s.index("hipError_t vcap_decode_attention_dispatch", a0)
+    att = s[a0:a1]
+    att = att.replace("  __shared__ float s_p[4][64];\n", "  __shared__ float s_p[4][64];\n  const unsigned long long t0 = VCAP_RT();\n", 1)
+    att = att.replace("  if (kg == 0) {\n    const float inv = 1.0f / sum;",
+                      "  const unsigned long long t2 = VCAP_RT();\n  if (kg == 0) {\n    const float inv = 1.0f / sum;", 1)
+    att = att[:att.rindex("}")] + "  if (threadIdx.x == 0) vcap_stamp_rec(0xA000ull, t0, t0, t2, t2, VCAP_RT());\n}\n\n"
+    s = s[:a0] + att + s[a1:]
+    return s
+
+
+def main():
+    tmp = Path("/tmp/vcap_stamps_build")
+    shutil.rmtree(tmp, ignore_errors=True)
+    src = tmp / "pkg" / "csrc"  # runtime.hip includes ../../include/vcap.h
+    src.mkdir(parents=True)
+    (tmp / "obj").mkdir()
+    shutil.copytree(ROOT / "include", tmp / "include")
+    for f in SRC.iterdir():
+        shutil.copy(f, src / f.name)
+    p = src / "decode.hip"
+    p.write_text(patch_decode(p.read_text()))
+    flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-munsafe-fp-atomics", "-Wno-unused-result",
+             f"-I{src}", f"-I{ROOT / 'include'}"]
+    procs = []
+    for f in sorted(src.glob("*.hip")):
+        extra = ["-fno-honor-nans"] if f.name == "vit_attention.hip" else []
+        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", *flags, *extra, "-c", str(f), "-o",
+                                       str(tmp / "obj" / (f.stem + ".o"))]))
+    if any(p.wait() for p in procs):
+        sys.exit("compile failed")
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(OUT),
+                           *map(str, sorted((tmp / "obj").glob("*.o")))])
+    print(OUT)
+
+
+if __name__ == "__main__":
+    main()

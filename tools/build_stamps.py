@@ -16,17 +16,21 @@ ROOT = Path(__file__).resolve().parents[1]
 SRC = ROOT / "video-caption-algorithm_amd" / "csrc"
 OUT = ROOT / "video-caption-algorithm_amd" / "vcap" / "_lib" / "libvcap_stamps.so"
 
-HEADER = r'''
+HEADER_T = r'''
 __device__ unsigned long long g_vcap_stamps[8 << 18];
 __device__ unsigned int g_vcap_stamp_n;
+#ifndef VCAP_RT
 #define VCAP_RT() ({ asm volatile("" ::: "memory"); unsigned long long _t = __builtin_amdgcn_s_memrealtime(); asm volatile("" ::: "memory"); _t; })
+#endif
 __device__ __forceinline__ void vcap_stamp_rec(unsigned long long tag, unsigned long long t0, unsigned long long t1,
                                                unsigned long long t2, unsigned long long t3, unsigned long long t4) {
   const unsigned i = atomicAdd(&g_vcap_stamp_n, 1u);
   if (i < (1u << 18)) {
     unsigned long long* r = g_vcap_stamps + 8ull * i;
     r[0] = tag; r[1] = blockIdx.x | ((unsigned long long)gridDim.x << 20) | ((unsigned long long)blockIdx.y << 40);
-    r[2] = t0; r[3] = t1; r[4] = t2; r[5] = t3; r[6] = t4; r[7] = 0;
+    r[2] = t0; r[3] = t1; r[4] = t2; r[5] = t3; r[6] = t4;
+    r[7] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+           ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);  // HW_ID | XCC_ID
   }
 }
 extern "C" __attribute__((visibility("default"))) int vcap_diag_stamps(void* host, int max_rec) {
@@ -45,8 +49,14 @@ extern "C" __attribute__((visibility("default"))) int vcap_diag_stamps(void* hos
 '''
 
 
+def header(sfx: str) -> str:
+    # one buffer + reader per translation unit (device globals are per code object)
+    return (HEADER_T.replace("g_vcap_stamps", "g_vcap_stamps" + sfx).replace("g_vcap_stamp_n", "g_vcap_stamp_n" + sfx)
+            .replace("vcap_stamp_rec", "vcap_stamp_rec" + sfx).replace("vcap_diag_stamps", "vcap_diag_stamps" + sfx))
+
+
 def patch_decode(s: str) -> str:
-    s = s.replace('#include "vcap_kernels.h"\n', '#include "vcap_kernels.h"\n' + HEADER, 1)
+    s = s.replace('#include "vcap_kernels.h"\n', '#include "vcap_kernels.h"\n' + header(""), 1)
     # GEMV kernel
     k0 = s.index("__global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {")
     k1 = s.index("// General rows kernel", k0)
@@ -74,6 +84,20 @@ def patch_decode(s: str) -> str:
     return s
 
 
+def patch_attention(s: str) -> str:
+    s = s.replace('#include "vcap_kernels.h"\n', '#include "vcap_kernels.h"\n' + header("_attn"), 1)
+    k0 = s.index("void vcap_vit_attention_bf16_kernel(")
+    ends = [s.find(m, k0) for m in ("// Persistent walk over", "template <int KT, int KE, int WAVES, bool MXO>\nstatic hipError_t launch_attn_bf16")]
+    k1 = min(e for e in ends if e > 0)
+    b = s[k0:k1]
+    b = b.replace("  const int fr = lane & 15, fg = lane >> 4;\n", "  const int fr = lane & 15, fg = lane >> 4;\n  const unsigned long long t0 = VCAP_RT();\n", 1)
+    b = b.replace('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n  __syncthreads();\n',
+                  '  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n  __syncthreads();\n  const unsigned long long t1 = VCAP_RT();\n', 1)
+    b = b[:b.rindex("}")] + "  __syncthreads();\n  if (threadIdx.x == 0) vcap_stamp_rec_attn(0xB000ull | KT, t0, t1, VCAP_RT(), 0, 0);\n}\n\n"
+    assert b.count("VCAP_RT()") == 3
+    return s[:k0] + b + s[k1:]
+
+
 def main():
     tmp = Path("/tmp/vcap_stamps_build")
     shutil.rmtree(tmp, ignore_errors=True)
@@ -85,6 +109,8 @@ def main():
         shutil.copy(f, src / f.name)
     p = src / "decode.hip"
     p.write_text(patch_decode(p.read_text()))
+    p = src / "vit_attention.hip"
+    p.write_text(patch_attention(p.read_text()))
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-munsafe-fp-atomics", "-Wno-unused-result",
              f"-I{src}", f"-I{ROOT / 'include'}"]
     procs = []

@@ -196,6 +196,13 @@ struct ProcToks {
   }
 };
 
+// A 32-row PRO_DIRECT GEMV (two 16-row tiles) whose A fragments of both tiles would not fit beside
+// its weight fragments (> 64 x 16 B per lane) keeps one row tile of A live at a time.
+template <typename T, int MT, int NTB, int PRO, int NSL>
+constexpr bool gemv_stream_a() {
+  return PRO == PRO_DIRECT && MT == 2 && NSL * (NTB + MT) > 64;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Decode GEMV (M <= 32 rows): everything a workgroup needs from memory is issued at kernel start,
 // in the order it is consumed (vmcnt retires in issue order):
@@ -228,12 +235,16 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
 
   if constexpr (EPI == EPI_LOGITS) proc_flags_zero<MP, NTB>(s_rep, s_ban);
 
-  // ---- 1) activation operand
-  u32x4 af[PRO == PRO_DIRECT ? MT : 1][PRO == PRO_DIRECT ? NSL : 1];
+  // ---- 1) activation operand (STREAM_A: row tile 0 only; tile 1 is loaded into the same registers
+  // as the tile-0 MFMAs consume them, so the per-row MFMA order - and every output bit - is that of
+  // the all-tiles-live form)
+  constexpr bool STREAM_A = gemv_stream_a<T, MT, NTB, PRO, NSL>();
+  constexpr int MTA = STREAM_A ? 1 : MT;  // row tiles of A fragments live at once
+  u32x4 af[PRO == PRO_DIRECT ? MTA : 1][PRO == PRO_DIRECT ? NSL : 1];
   f32x4 xv[PRO == PRO_LN ? RPW : 1][KC > 0 ? KC : 1], gv[KC > 0 ? KC : 1], bv[KC > 0 ? KC : 1];
   if constexpr (PRO == PRO_DIRECT) {
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
+    for (int i = 0; i < MTA; ++i) {
       const long xo = (long)min(m0 + i * 16 + fr, M - 1) * a.ldx + fg * E;
 #pragma unroll
       for (int s = 0; s < NSL; ++s) af[i][s] = vcap_dec_aload(a.x, (xo + (g0 + s) * KS) * (long)sizeof(T));
@@ -252,7 +263,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
     }
   }
 
-  if constexpr (PRO == PRO_LN || NSL * (NTB + MT) < 64)
+  if constexpr (PRO == PRO_LN || NSL * (NTB + MTA) < 64)
     asm volatile("" ::: "memory");  // the activation loads issue (and retire) before the weights
   // ---- 2) weights
   u32x4 wf[NSL][NTB];
@@ -289,7 +300,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
     for (int r = 0; r < RPW; ++r)
 #pragma unroll
       for (int c = 0; c < KC; ++c) asm volatile("" : "+v"(xv[r][c])::"memory");
-  } else if constexpr (NSL * (NTB + MT) < 64) {  // (at the 64-fragment budget: let the compiler stream)
+  } else if constexpr (NSL * (NTB + MTA) < 64) {  // (at the 64-fragment budget: let the compiler stream)
     asm volatile("" : "+v"(af[0][0])::"memory");
   }
 
@@ -332,6 +343,19 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NTB; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if constexpr (STREAM_A) {
+    const long xo1 = (long)min(m0 + 16 + fr, M - 1) * a.ldx + fg * E;
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) acc[0][j] = mfma_frag(af[0][s], wf[s][j], acc[0][j], (T*)nullptr);
+      af[0][s] = vcap_dec_aload(a.x, (xo1 + (g0 + s) * KS) * (long)sizeof(T));
+    }
+#pragma unroll
+    for (int s = 0; s < NSL; ++s)
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) acc[MT - 1][j] = mfma_frag(af[0][s], wf[s][j], acc[MT - 1][j], (T*)nullptr);
+  } else
 #pragma unroll
   for (int s = 0; s < NSL; ++s) {
 #pragma unroll
@@ -773,11 +797,13 @@ constexpr bool gemv_nsl_ok(int nsl) {
   return sizeof(T) == 2 ? (nsl == 6 || nsl == 8 || nsl == 24 || nsl == 32) : (nsl == 12 || nsl == 16);
 }
 // register budget: NSL x (NTB weight + MT activation) 16-byte fragments held at once
+// (a 32-row PRO_DIRECT GEMV whose two row tiles of A fragments do not fit beside the weights streams
+// them: one row tile live at a time, gemv_stream_a above the kernel)
 template <typename T, int MT, int NTB, int PRO, int NSL>
 constexpr bool gemv_fits() {
   constexpr int KS = 4 * Frag<T>::kElems;
-  return gemv_nsl_ok<T>(NSL) && NSL * (NTB + (PRO == PRO_DIRECT ? MT : 0)) <= 64 &&
-         (PRO != PRO_LN || NSL * KS * 4 <= 1024);
+  constexpr int live_a = PRO != PRO_DIRECT ? 0 : gemv_stream_a<T, MT, NTB, PRO, NSL>() ? 1 : MT;
+  return gemv_nsl_ok<T>(NSL) && NSL * (NTB + live_a) <= 64 && (PRO != PRO_LN || NSL * KS * 4 <= 1024);
 }
 
 // Raise a kernel's dynamic-LDS limit once to what the CU has left beside its static LDS; returns

@@ -24,7 +24,8 @@ with torch.cuda.stream(s):
     res = {}
     for mx in (lo, hi):
         if beams == 1:
-            cfg = GenConfig(mx, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, True)
+            cfg = GenConfig(mx, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, True,
+                            max_blocks=int(os.environ.get("CAP", "0")))
             run = lambda: dec.generate_ids(pre, [ga.bos_token_id], cfg)
         else:
             run = lambda: search.beam_search_device(dec, pre, [ga.bos_token_id], num_beams=beams, max_new_tokens=mx,
@@ -38,5 +39,5 @@ with torch.cuda.stream(s):
             run()
         torch.cuda.synchronize()
         res[mx] = (time.perf_counter() - t) / 10 * 1e3
-print(f"{Path(os.environ.get('VCAP_LIB', 'base')).name} {name} B={B} beams={beams}: "
+print(f"{Path(os.environ.get('VCAP_LIB', 'base')).name} {name} B={B} beams={beams} cap={os.environ.get('CAP', '0')}: "
       f"step {(res[hi]-res[lo])/(hi-lo)*1e3:.1f} us first {res[lo]*1e3:.0f} us")

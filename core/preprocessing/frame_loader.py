@@ -1,9 +1,11 @@
 """frames_dir -> [1, T, 3, H, W] tensor (behaviour of reference core/preprocessing/frame_loader.py:13-49).
 
-Strided pick files[::max(n // T, 1)][:T] of sorted frame_*.jpg, decoded by PIL on the host; the
-Resize((S, S)) -> ToTensor -> Normalize chain runs on the GPU (vcap.preprocess, bit-identical to
-PIL's BILINEAR resample + the f32 normalisation) for a cuda `device`.  `backend="pil"` keeps the
-per-frame host chain (PIL resize + numpy), e.g. for a CPU-only caller.  torchvision is not required.
+Strided pick files[::max(n // T, 1)][:T] of sorted frame_*.jpg.  For a cuda `device` the frames are
+decoded on the GPU (vcap.jpeg: host entropy decode, device IDCT / upsampling / YCbCr -> RGB,
+bit-identical to PIL's Image.open(...).convert("RGB")) and the Resize((S, S)) -> ToTensor ->
+Normalize chain runs there too (vcap.preprocess, bit-identical to PIL's BILINEAR resample + the f32
+normalisation).  `backend="pil"` keeps the per-frame host chain (PIL decode + resize + numpy), e.g.
+for a CPU-only caller or a JPEG kind the GPU decoder refuses.  torchvision is not required.
 """
 from __future__ import annotations
 
@@ -41,16 +43,16 @@ def load_video_tensor(frames_dir, num_frames: int, image_size: int, device: str 
         backend = "hip" if on_gpu else "pil"
     if backend not in ("hip", "pil"):
         raise ValueError(f"backend must be 'auto', 'hip' or 'pil', got {backend!r}")
-    decoded = []
-    for p in picks:
-        with Image.open(p) as im:
-            decoded.append(np.asarray(im.convert("RGB")) if backend == "hip" else _to_chw(im, image_size))
     if backend == "hip":
-        from vcap.preprocess import frames_to_video
-        if len({d.shape for d in decoded}) != 1:
-            raise ValueError("frames of one video must share one size")
-        video = frames_to_video(decoded, image_size, device)
+        from vcap.jpeg import decode_jpegs
+        from vcap.preprocess import preprocess_frames
+        blobs = [Path(p).read_bytes() for p in picks]
+        video = preprocess_frames(decode_jpegs(blobs, device), image_size).unsqueeze(0)
     else:
+        decoded = []
+        for p in picks:
+            with Image.open(p) as im:
+                decoded.append(_to_chw(im, image_size))
         video = torch.from_numpy(np.stack(decoded)[None]).to(device)
     log.info("frames_dir=%s total=%s sampled=%s", frames_dir, len(files), len(picks))
     return video

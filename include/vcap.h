@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 8
+#define VCAP_ABI_VERSION 9
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -156,6 +156,20 @@ size_t vcap_frames_workspace_bytes(int n, int in_h, int in_w, int out_h, int out
 int vcap_frames_preprocess(const uint8_t* frames, int n, int in_h, int in_w, int out_h, int out_w, const float* mean3,
                            const float* std3, float* out, uint8_t* out_u8, void* workspace, size_t ws_bytes,
                            void* stream);
+
+/* ---- JPEG frame decode (core/preprocessing/frame_loader.py:42-44: PIL Image.open(path).convert("RGB"),
+ *      i.e. libjpeg-turbo's default decompression) for baseline sequential Huffman JPEGs: 8-bit, 1 or
+ *      3 components in one interleaved scan, 4:4:4 / 4:2:2 / 4:2:0, restart markers.  The host
+ *      parses and entropy-decodes (parallel threads, one image each); the device dequantises and runs
+ *      jpeg_idct_islow, fancy-upsamples chroma and converts YCbCr -> RGB with libjpeg's fixed-point
+ *      arithmetic, bit-identical to Pillow.  Progressive / arithmetic-coded / 12-bit / CMYK images ->
+ *      VCAP_E_UNSUPPORTED.  vcap_jpeg_decode_batch: n images (HOST byte buffers) that share size,
+ *      sampling and quantisation tables -> out uint8 [n, H, W, 3] (device); returns after the device
+ *      work of the call has finished (the host coefficient staging is released). ---- */
+int vcap_jpeg_probe(const uint8_t* data, size_t len, int* width, int* height, int* comps);
+size_t vcap_jpeg_workspace_bytes(const uint8_t* data, size_t len, int n);
+int vcap_jpeg_decode_batch(const uint8_t* const* data, const size_t* lens, int n, uint8_t* out, void* workspace,
+                           size_t ws_bytes, void* stream);
 
 /* ---- MXFP8 (BASELINE configs[4]: fp8 MFMA path for the ViT GEMMs) ----
  * vcap_mx_quantize: rows of f32 / bf16 [rows, K] (row stride ldx) -> e4m3 [rows, K] + scales.

@@ -684,6 +684,36 @@ int vcap_frames_preprocess(const uint8_t* frames, int n, int in_h, int in_w, int
   return 0;
 }
 
+int vcap_jpeg_probe(const uint8_t* data, size_t len, int* width, int* height, int* comps) {
+  if (!data || !len) return fail(VCAP_E_ARG, "vcap_jpeg_probe: bad arguments");
+  JpegInfo f;
+  std::string e;
+  if (int rc = vcap_jpeg_header(data, len, &f, &e)) return fail(rc, "vcap_jpeg_probe: " + e);
+  if (width) *width = f.width;
+  if (height) *height = f.height;
+  if (comps) *comps = f.ncomp;
+  return 0;
+}
+
+size_t vcap_jpeg_workspace_bytes(const uint8_t* data, size_t len, int n) {
+  JpegInfo f;
+  std::string e;
+  if (!data || !len || n <= 0 || vcap_jpeg_header(data, len, &f, &e)) return 0;
+  return vcap_jpeg_ws_bytes(f, n);
+}
+
+int vcap_jpeg_decode_batch(const uint8_t* const* data, const size_t* lens, int n, uint8_t* out, void* workspace,
+                           size_t ws_bytes, void* stream) {
+  if (!data || !lens || n <= 0 || !out || !workspace) return fail(VCAP_E_ARG, "vcap_jpeg_decode_batch: bad arguments");
+  for (int i = 0; i < n; ++i)
+    if (!data[i] || !lens[i]) return fail(VCAP_E_ARG, "vcap_jpeg_decode_batch: empty image buffer");
+  std::string e;
+  if (int rc = vcap_jpeg_decode(data, lens, n, out, workspace, ws_bytes, (hipStream_t)stream, &e))
+    return fail(rc, "vcap_jpeg_decode_batch: " + e);
+  g_err.clear();
+  return 0;
+}
+
 static int ensure_attn_lds() {
   if (attn_lds_configured) return 0;
   attn_lds_configured = true;

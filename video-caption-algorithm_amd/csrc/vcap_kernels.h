@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 struct GemmEpi {
   const float* bias;  // [N] or nullptr
   const float* res;   // residual source (f32) or nullptr
@@ -163,3 +165,15 @@ size_t vcap_frames_ws_bytes(int n, int in_h, int in_w, int out_h, int out_w);
 hipError_t vcap_frames_preprocess_dispatch(const uint8_t* frames, int n, int in_h, int in_w, int out_h, int out_w,
                                            const float* mean3, const float* std3, float* out, uint8_t* out_u8,
                                            void* ws, hipStream_t s);
+
+// JPEG frame decode (jpeg.hip): header of one baseline image, workspace of n same-shape images,
+// host entropy decode + device IDCT / upsampling / colour conversion into uint8 [n, H, W, 3].
+struct JpegInfo {
+  int width = 0, height = 0, ncomp = 0, hmax = 1, vmax = 1;
+  int id[3] = {0, 0, 0}, h[3] = {1, 1, 1}, v[3] = {1, 1, 1};
+  int bx[3] = {0, 0, 0}, by[3] = {0, 0, 0};  // block grid per component, padded to whole MCUs
+};
+int vcap_jpeg_header(const uint8_t* data, size_t len, JpegInfo* info, std::string* err);
+size_t vcap_jpeg_ws_bytes(const JpegInfo& f, int n);
+int vcap_jpeg_decode(const uint8_t* const* data, const size_t* lens, int n, uint8_t* out, void* ws, size_t ws_bytes,
+                     hipStream_t s, std::string* err);

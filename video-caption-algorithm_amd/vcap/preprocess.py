@@ -3,8 +3,8 @@
 Replaces the per-frame host transform chain of core/preprocessing/frame_loader.py:34-45
 (torchvision Resize((S, S)) -> ToTensor -> Normalize) with one upload of the uint8 frames and three
 kernels (weights, horizontal pass, vertical pass + normalise), bit-identical to PIL's BILINEAR
-resample and the reference's f32 normalisation.  JPEG decode stays on the host (PIL), as in the
-reference.  There is no host fallback: a missing libvcap_hip.so raises.
+resample and the reference's f32 normalisation.  The JPEG decode in front of it is vcap.jpeg (also on
+the GPU).  There is no host fallback: a missing libvcap_hip.so raises.
 """
 from __future__ import annotations
 

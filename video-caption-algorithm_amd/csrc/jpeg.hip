@@ -122,6 +122,7 @@ int parse(const uint8_t* d, size_t len, Parsed& p, std::string& err) {
       f.ncomp = s[5];
       if (f.ncomp != 1 && f.ncomp != 3) return bad("1 or 3 components only");
       if (sl < 6 + 3 * (size_t)f.ncomp || f.width <= 0 || f.height <= 0) return bad("SOF length");
+      if ((long)f.width * f.height > (64L << 20)) return bad("image larger than 64 Mpixel");
       f.hmax = f.vmax = 1;
       for (int k = 0; k < f.ncomp; ++k) {
         f.id[k] = s[6 + 3 * k];
@@ -239,7 +240,7 @@ struct BitReader {
     return 0;  // corrupt code: libjpeg warns and continues with zeros
   }
   int receive_extend(int s) {
-    if (s == 0) return 0;
+    if (s <= 0 || s > 16) return 0;  // (a corrupt DC table can name > 16 bits: zeros, as libjpeg warns)
     fill();
     const int v = (int)peek(s);
     skip(s);
@@ -489,6 +490,10 @@ int vcap_jpeg_decode(const uint8_t* const* data, const size_t* lens, int n, uint
     }
   }
   const JpegInfo& f = ps[0].info;
+  if ((long)n * f.width * f.height > (1L << 31) / 3) {
+    *err = "batch larger than 2 GiB of RGB";
+    return VCAP_E_UNSUPPORTED;
+  }
   if (ws_bytes < vcap_jpeg_ws_bytes(f, n)) {
     *err = "workspace too small";
     return VCAP_E_WORKSPACE;

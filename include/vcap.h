@@ -176,7 +176,8 @@ int vcap_jpeg_decode_batch(const uint8_t* const* data, const size_t* lens, int n
  * vcap_layernorm_mx: LayerNorm (f32 rows) fused with the quantisation of its output.
  * vcap_gemm_mx: C = epi(A . W^T) with A [M, K], W [N, K] MXFP8 (contiguous rows, K % 256 == 0);
  *   out_dtype BF16 / F32 (res != NULL: C += ..., in place, f32) or MXFP8 (act must be 1 = bias +
- *   GELU-tanh, C e4m3 [M, N] + c_scales, N % 128 == 0). */
+ *   GELU-tanh, C e4m3 [M, N] + c_scales (8-byte aligned, vcap_mx_scale_bytes(M, N) bytes: the
+ *   padding rows of the last 256-row group are written too), N % 128 == 0). */
 size_t vcap_mx_scale_bytes(int rows, int K);
 /* bf16 qkv [frames*tokens, 3*heads*64] -> attention output in MXFP8 ([frames*tokens, heads*64] e4m3 +
  * scales), the A operand of an MXFP8 attn-proj GEMM */

@@ -101,7 +101,11 @@ VCAP_DEV void epilogue256(const f32x4 (&acc)[2][2][4][2], int m0, int n0, int wr
   if constexpr (EPI == 4) {
     // bias + GELU, re-quantised to MXFP8 for the next GEMM: the 32-column block
     // n0 + wc*64 + qn*32 of row m lives in this lane (j = 0, 1) and the lanes fg = 0..3 of the
-    // same fr, so its max |x| is a 2-step permlane reduction.
+    // same fr, so its max |x| is a 2-step permlane reduction.  The scale bytes of one lane's 8 row
+    // blocks (qm, i + h) of a column block are adjacent in the mx_scale_index layout (row bits
+    // 4..7 are its fastest index): they are collected in a register and stored as one u64 per
+    // (lane, qn) instead of 8 scattered byte stores.
+    uint64_t sc[2] = {0, 0};
 #pragma unroll
     for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
@@ -136,7 +140,8 @@ VCAP_DEV void epilogue256(const f32x4 (&acc)[2][2][4][2], int m0, int n0, int wr
             const f32x4 q0 = v[0] * inv, q1 = v[1] * inv;
             x[2 * h] = pack_fp8x4(q0.x, q0.y, q0.z, q0.w);
             x[2 * h + 1] = pack_fp8x4(q1.x, q1.y, q1.z, q1.w);
-            if (fg == 0 && m < M && nb < N) epi.c_scale[mx_scale_index(m, nb, (M + 255) >> 8)] = (uint8_t)sbyte;
+            (void)m;
+            sc[qn] |= (uint64_t)(uint32_t)sbyte << (8 * (qm * 4 + i + h));
           }
           transpose4_groups(x);
           const int ms = m0 + wr * 128 + qm * 64 + (i + (fg >> 1)) * 16 + fr;
@@ -145,6 +150,14 @@ VCAP_DEV void epilogue256(const f32x4 (&acc)[2][2][4][2], int m0, int n0, int wr
                       (u32x4){x[0], x[1], x[2], x[3]});
         }
       }
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn) {
+      const int nb = n0 + wc * 64 + qn * 32;
+      // rows m0 + wr*128 + fr + 16 * (qm * 4 + i + h): byte (qm * 4 + i + h) of sc[qn]; rows past M
+      // land in the scale buffer's padding of the last 256-row group
+      if (fg == 0 && nb < N)
+        *reinterpret_cast<uint64_t*>(epi.c_scale + mx_scale_index(m0 + wr * 128 + fr, nb, (M + 255) >> 8)) = sc[qn];
+    }
   } else if (sizeof(TOut) == 2 && (EPI == 0 || EPI == 1) && (N & 31) == 0 && (ldc & 7) == 0 &&
              ((uintptr_t)C & 15) == 0) {
     // bf16 out, 16-byte stores: lanes fg and fg ^ 1 (lane ^ 16) trade halves so the even lane

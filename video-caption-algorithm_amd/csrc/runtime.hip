@@ -652,6 +652,8 @@ int vcap_gemm_mx(const void* A, const uint8_t* a_scales, const void* W, const ui
   if (out_dtype == VCAP_DT_MXFP8) {
     if (act != 1 || !bias || !c_scales || res || N % 128)
       return fail(VCAP_E_UNSUPPORTED, "vcap_gemm_mx: MXFP8 output needs bias + gelu (act=1), c_scales, N % 128 == 0");
+    if (reinterpret_cast<uintptr_t>(c_scales) % 8)
+      return fail(VCAP_E_ARG, "vcap_gemm_mx: c_scales must be 8-byte aligned");
   } else if (out_dtype != VCAP_DT_BF16 && out_dtype != VCAP_DT_F32) {
     return fail(VCAP_E_ARG, "vcap_gemm_mx: out_dtype");
   }

@@ -68,8 +68,10 @@ def parse():
                          "-1 = auto: 32 with two-batch encodes, else 0 - profiles/r02_decode_experiments.txt)")
     ap.add_argument("--decode-blocks", type=int, default=96,
                     help="cap the decode GEMV grids near this many workgroups (0 = whole-chip grids)")
-    ap.add_argument("--dec-lanes", type=int, default=2,
-                    help="decodes in flight at once (own stream + workspace + graph each)")
+    ap.add_argument("--dec-lanes", type=int, default=0,
+                    help="decodes in flight at once (own stream + workspace + graph each); 0 = auto: 3 for beam "
+                         "search (configs[3]: +2.3 %%, 4 streams = the box's 4 hardware queues; "
+                         "profiles/r03_c3_schedule_sweep.txt), else 2")
     ap.add_argument("--dec-group", type=int, default=2,
                     help="consecutive batches decoded together as one decode of group*batch rows")
     ap.add_argument("--enc-group", type=int, default=0,
@@ -290,6 +292,8 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
+    if args.dec_lanes <= 0:
+        args.dec_lanes = 3 if args.beams > 1 else 2
     if args.enc_group <= 0:
         args.enc_group = 2 if args.batch * args.frames <= 128 and args.dec_group % 2 == 0 else 1
     if args.reserve_cus < 0:

@@ -102,6 +102,16 @@ def test_library_exports_every_header_symbol():
     assert lib.vcap_abi_version() == N.ABI_VERSION
 
 
+def test_gemm_mx_argument_checks_without_gpu():
+    """vcap_gemm_mx refuses an MXFP8 output whose scale buffer is not 8-byte aligned (the epilogue
+    stores 8 scale bytes at once) before touching the device; placeholder pointers are never read."""
+    lib = N.lib()
+    args = (16, 16, 16, 16, N.DT_MXFP8, 16, 128)
+    assert lib.vcap_gemm_mx(*args, 17, 256, 128, 256, 16, 1, None, None) == N.E_ARG
+    assert b"8-byte aligned" in lib.vcap_last_error()
+    assert lib.vcap_gemm_mx(*args, 16, 256, 128, 256, 16, 0, None, None) == N.E_UNSUPPORTED  # MXFP8 out needs GELU
+
+
 def test_workspace_queries_without_gpu():
     import ctypes as C
     va, ga = configs.vit_arch("vit_base_patch16_224"), configs.gpt2_arch("gpt2")

@@ -89,6 +89,16 @@ def parse():
                     help="skip the fp32 agreement check of the last timed batch")
     ap.add_argument("--no-decode-alone", dest="decode_alone", action="store_false",
                     help="skip the decode-step-alone measurement")
+    ap.add_argument("--strict-steps", type=int, default=40,
+                    help="batches timed in the strict_batch leg (one batch of --batch videos per encode and per "
+                         "decode, no coalescing; 0 disables)")
+    ap.add_argument("--batch-sizes", default="",
+                    help="comma list (the reference's --batch-sizes sweep, core/scripts/benchmark_baseline.py:"
+                         "486-493): time the default schedule and the strict per-batch schedule at each batch size")
+    ap.add_argument("--sweep-steps", type=int, default=24, help="batches timed per --batch-sizes point")
+    ap.add_argument("--dump-ids", default="",
+                    help="rank 0 saves every timed batch's ids (gathered over ranks: [world*steps, B, max_new]) "
+                         "to this .npy path")
     return ap.parse_args()
 
 
@@ -257,6 +267,44 @@ def parity_report(sd, va, ga, video, pre, enc, dec, cfg, last, dev):
     return rep
 
 
+def time_schedule(enc, pre, dec, cfg, video, prompt, dev, world, steps, warmup, **sched):
+    """Time `steps` batches of `video` through a fresh CaptionPipeline with the given schedule,
+    bracketed like the headline (synchronize + barrier on both sides, max over ranks): captions/s,
+    per-batch latency stats (encode start -> ids) and B / p50."""
+    import torch
+    import torch.distributed as dist
+    from vcap.pipeline import CaptionPipeline
+    B = video.shape[0]
+    pipe = CaptionPipeline(enc, pre, dec, cfg, B, prompt, dev, **sched)
+    try:
+        for _ in range(max(warmup, 1)):
+            pipe.submit(video)
+        pipe.synchronize()
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            pipe.submit(video, starts[k], None, ends[k])
+        pipe.synchronize()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        elapsed = float(el.item())
+        lat = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    finally:
+        pipe.close()
+    p50 = statistics.median(lat)
+    return {"value": world * B * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
+            "p50_latency_ms": p50, "captions_per_s_b_over_p50": world * B / (p50 / 1e3),
+            "latency_ms_stats": describe(lat)}
+
+
 def workload_tag(args, world):
     if args.precision == "fp8":
         return "configs[4]-shaped, MXFP8 ViT GEMMs"
@@ -328,7 +376,8 @@ def main():
                 ids_all[t].copy_(ids[i * B:(i + 1) * B])
         return ids
 
-    pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev, gather=keep if world > 1 else None,
+    pipe = CaptionPipeline(enc, pre, dec, cfg, B, [ga.bos_token_id], dev,
+                           gather=keep if (world > 1 or args.dump_ids) else None,
                            reserve_cus=0 if args.serial else args.reserve_cus,
                            dec_lanes=1 if args.serial else args.dec_lanes,
                            confine_decode=args.confine_decode and not args.serial,
@@ -398,8 +447,39 @@ def main():
         torch.cuda.synchronize(dev)
         del ids_host, pinned, vid_h
 
+    if args.dump_ids and rank == 0:
+        np.save(args.dump_ids, (gathered if world > 1 else ids_all).cpu().numpy())
+
     # caption lengths of the last timed batch (new tokens up to and including EOS)
     last = pipe.result(pipe.last_slot).cpu()
+    pipe.synchronize()
+    prompt = [ga.bos_token_id]
+    # strict_batch: what a caller with ONE batch of B videos sees - one B-video encode and one B-row
+    # decode per batch (no two-batch coalescing), two decode lanes, timed like `value`
+    strict = None
+    if args.strict_steps > 0 and not args.serial:
+        strict = time_schedule(enc, pre, dec, cfg, video, prompt, dev, world, args.strict_steps, args.warmup,
+                               dec_lanes=args.dec_lanes, dec_group=1, enc_group=1, reserve_cus=0)
+        strict["schedule"] = (f"one {B}-video encode + one {B}-row decode graph per batch, {args.dec_lanes} decode "
+                              f"lanes, no coalescing")
+    sweep = None
+    if args.batch_sizes:
+        sweep = []
+        for bs in [int(x) for x in args.batch_sizes.split(",") if x]:
+            vid = torch.from_numpy(prng.imagenet_frames(2000 + bs, (bs, T, 3, va.image, va.image))).to(dev)
+            eg = 2 if bs * T <= 128 and args.dec_group % 2 == 0 else 1
+            pt = {"batch": bs}
+            pt["default_schedule"] = time_schedule(enc, pre, dec, cfg, vid, prompt, dev, world, args.sweep_steps,
+                                                   args.warmup, dec_lanes=args.dec_lanes, dec_group=args.dec_group,
+                                                   enc_group=eg, reserve_cus=32 if eg == 2 else 0)
+            pt["strict_batch"] = time_schedule(enc, pre, dec, cfg, vid, prompt, dev, world, args.sweep_steps,
+                                               args.warmup, dec_lanes=args.dec_lanes, dec_group=1, enc_group=1,
+                                               reserve_cus=0)
+            for k in ("default_schedule", "strict_batch"):
+                pt[k].pop("latency_ms_stats")
+            sweep.append(pt)
+            del vid
+        torch.cuda.empty_cache()
     # parity of what was timed (outside the timed region): the last batch's ids against the fp32
     # parity mode (token-exact against the reference: tests/test_gpu_parity.py) on the same frames,
     # with the near-tie evidence for every divergent caption (vcap/fidelity.py)
@@ -518,6 +598,8 @@ def main():
             "path_roofline": {"t_roof_ms": t_roof * 1e3, "t_measured_ms": elapsed / args.steps * 1e3,
                               "frac": t_roof / (elapsed / args.steps),
                               "vit_tflop": vit_exec / 1e12, "decode_weight_gb": dec_bytes / 1e9},
+            "strict_batch": strict,
+            "batch_sweep": sweep,
             "pmc": pmc_summary(args.vit, args.gpt2, M, args.precision),
             "parity": parity,
             "decode_roofline": dec_alone,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 9
+#define VCAP_ABI_VERSION 10
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -119,6 +119,11 @@ typedef struct vcap_gen_params {
   int max_blocks;            /* 0: whole-chip grids; > 0: cap the projection GEMV grids near this
                                 many workgroups (wider tiles per workgroup) - for a decode that
                                 shares the GPU with an encode holding most CUs */
+  int persistent;            /* greedy bf16 decodes of <= 16 rows: 0 = one launch per decode kernel
+                                (~62 per token step); > 0 = steps 1.. as ONE persistent launch of
+                                this many workgroups, one per CU (csrc/decode_persist.hip, ids and
+                                logits bit-identical); < 0 = auto (VCAP_PERSIST_G or 128).  Other
+                                decodes ignore it. */
 } vcap_gen_params;
 
 const char* vcap_last_error(void);
@@ -163,9 +168,12 @@ int vcap_frames_preprocess(const uint8_t* frames, int n, int in_h, int in_w, int
  *      parses and entropy-decodes (parallel threads, one image each); the device dequantises and runs
  *      jpeg_idct_islow, fancy-upsamples chroma and converts YCbCr -> RGB with libjpeg's fixed-point
  *      arithmetic, bit-identical to Pillow.  Progressive / arithmetic-coded / 12-bit / CMYK images ->
- *      VCAP_E_UNSUPPORTED.  vcap_jpeg_decode_batch: n images (HOST byte buffers) that share size,
- *      sampling and quantisation tables -> out uint8 [n, H, W, 3] (device); returns after the device
- *      work of the call has finished (the host coefficient staging is released). ---- */
+ *      VCAP_E_UNSUPPORTED, and so are RGB-coded JPEGs (libjpeg's colour-space rule: no JFIF marker and
+ *      an Adobe transform of 0, or component ids 'R','G','B').  vcap_jpeg_decode_batch: n images (HOST
+ *      byte buffers) that share size and chroma sampling (each image keeps its own quantisation and
+ *      Huffman tables, as ffmpeg's per-frame MJPEG qscale writes them) -> out uint8 [n, H, W, 3]
+ *      (device); returns after the device work of the call has finished, on every path (the host
+ *      coefficient staging is released). ---- */
 int vcap_jpeg_probe(const uint8_t* data, size_t len, int* width, int* height, int* comps);
 size_t vcap_jpeg_workspace_bytes(const uint8_t* data, size_t len, int n);
 int vcap_jpeg_decode_batch(const uint8_t* const* data, const size_t* lens, int n, uint8_t* out, void* workspace,
@@ -231,6 +239,9 @@ int vcap_gpt2_sample(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const v
                      float* logits_out, float* warped_out, const int* force_ids, void* workspace, size_t ws_bytes,
                      void* stream);
 void vcap_graph_cache_clear(void);
+/* persistent-decode grid barriers that gave up (bounded spin, 0.5 s) since the library loaded: a
+ * nonzero value means some decode returned early and its ids are not valid (sticky counter). */
+unsigned vcap_decode_faults(void);
 /* number of instantiated decode graphs held by the cache (bounded LRU, VCAP_GRAPH_CACHE_MAX) */
 int vcap_graph_cache_size(void);
 /* decoder rows one call may carry: B * (prefix + prompt) at the prefill, B * num_beams per step */

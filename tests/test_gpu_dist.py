@@ -69,18 +69,40 @@ def test_caption_sharded_rccl_one_rank(tmp_path):
     assert res["world"] == 1 and np.array_equal(got[:, :exp.shape[1]], exp)
 
 
-def test_bench_two_ranks_gloo(tmp_path):
+def test_bench_two_ranks_gloo(tmp_path, device):
     """The N>1 bench path (torchrun, one process per rank, sharded videos, decode-lane id copies,
     ONE end-of-run all-gather, MAX-over-ranks timing) rehearsed with 2 ranks sharing the box's
-    GPU over gloo (VCAP_BENCH_DIST_BACKEND): rank 0 prints one JSON line for n_gpus = 2."""
+    GPU over gloo (VCAP_BENCH_DIST_BACKEND): rank 0 prints one JSON line for n_gpus = 2, and the
+    ids it gathered are, for every timed batch of every rank, the ids a single-process serial
+    bf16 run computes on that rank's frames (bench.py seeds rank r's videos with 1000 + r)."""
+    import torch
+    from vcap import configs, prng, weights
+    from vcap.model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder
+    steps = 4
+    dump = tmp_path / "ids.npy"
     env = dict(os.environ, VCAP_BENCH_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(HERE.parent / "bench.py"), "--gpus", "2",
-           "--steps", "4", "--warmup", "2", "--cpu-baseline-s", "0", "--no-parity", "--no-decode-alone",
-           "--host-e2e", "0"]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=160)
+           "--steps", str(steps), "--warmup", "2", "--cpu-baseline-s", "0", "--no-parity", "--no-decode-alone",
+           "--host-e2e", "0", "--strict-steps", "2", "--dump-ids", str(dump)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["global_batch"] == 16
+    assert d["strict_batch"]["value"] > 0
+    got = np.load(dump)
+    assert got.shape == (2 * steps, 8, 24)
+    va, ga = configs.vit_arch("vit_base_patch16_224"), configs.gpt2_arch("gpt2")
+    sd = weights.synthetic_state_dict(1, va, ga)
+    enc, pre = HipViTEncoder(sd, va, "bf16", device), HipPrefix(sd, ga.n_embd, device=device)
+    dec = HipGPT2Decoder(sd, ga, "bf16", device)
+    cfg = GenConfig(24, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, True)
+    cfg.max_blocks = 96
+    for rank in range(2):
+        video = torch.from_numpy(prng.imagenet_frames(1000 + rank, (8, 16, 3, va.image, va.image))).to(device)
+        _, prefix = enc.encode(video, pre)
+        exp = dec.generate_ids(prefix, [ga.bos_token_id], cfg).cpu().numpy()
+        for t in range(steps):
+            assert np.array_equal(got[rank * steps + t], exp), (rank, t)

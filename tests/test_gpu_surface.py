@@ -115,6 +115,44 @@ def test_device_sampling_warped_scores_match_hf_every_step(device, preset):
         torch.testing.assert_close(warped[s][fin], scores[s][fin], rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("preset", ["natural", "safe_sample"])
+def test_device_sampling_gpt2_vocab_matches_hf_every_step(device, preset):
+    """The same check at the full GPT-2 vocab (50,257 columns: the `vcap_sample_kernel<50>` instance
+    every `infer()` S3 candidate runs): replaying the reference engine's sampled history
+    (tests/golden/b16_b2_sample, make_goldens.py `sample_case`), at every step and row the device's
+    finite warped scores are exactly HF's TopK(50) -> TopP support (same token set) with values within
+    1e-4, and the raw logits match the reference's top-64 within 1e-3 (core/inference.py:12-15,
+    src/models/text_decoder.py:137-139)."""
+    from vcap.model import GenConfig, HipGPT2Decoder
+    meta, g, va, ga, sd, frames = case("b16_b2_sample")
+    kw = meta[preset]
+    ids = g[f"{preset}_ids"].astype(np.int64)
+    wi, wv = g[f"{preset}_warped_idx"], g[f"{preset}_warped_val"]
+    top_i, top_v = g[f"{preset}_top_i"], g[f"{preset}_top_v"]
+    steps, B, V = wi.shape[0], wi.shape[1], ga.vocab
+    assert V == 50257
+    L = kw["max_new_tokens"]
+    force = np.full((B, L), ga.eos_token_id, np.int64)
+    force[:, :ids.shape[1]] = ids
+    dec = HipGPT2Decoder(sd, ga, "fp32", device)
+    cfg = GenConfig(L, kw["min_new_tokens"], kw["no_repeat_ngram_size"], kw["repetition_penalty"], ga.eos_token_id,
+                    ga.eos_token_id, True, temperature=kw["temperature"], top_p=kw["top_p"], seed=11)
+    prefix = torch.from_numpy(g["inputs_embeds"][:, :4].copy()).to(device)
+    warped = torch.empty(L, B, V, device=device)
+    raw = torch.empty(L, B, V, device=device)
+    out = dec.generate_ids(prefix, [ga.bos_token_id], cfg, logits_out=raw, warped_out=warped,
+                           force_ids=torch.from_numpy(force))
+    assert np.array_equal(out.cpu().numpy()[:, :ids.shape[1]], ids)
+    warped, raw = warped.cpu().numpy(), raw.cpu().numpy()
+    for s in range(steps):
+        for b in range(B):
+            np.testing.assert_allclose(raw[s, b, top_i[s, b]], top_v[s, b], rtol=0, atol=1e-3)
+            keep = wi[s, b] >= 0
+            fin = np.flatnonzero(np.isfinite(warped[s, b]))
+            assert np.array_equal(fin, np.sort(wi[s, b][keep])), (s, b)
+            np.testing.assert_allclose(warped[s, b, wi[s, b][keep]], wv[s, b][keep], rtol=1e-5, atol=1e-4)
+
+
 def test_device_sampling_draws_follow_the_warped_distribution(device):
     """3200 first-token draws (100 rows x 32 seeds) of one prefix: every draw lies in the warped
     support, and the draw frequencies match softmax(warped scores) (chi-square, pooled bins)."""

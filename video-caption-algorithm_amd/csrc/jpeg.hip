@@ -44,6 +44,8 @@ struct Parsed {
   HuffTable dc[4], ac[4];
   int td[3], ta[3], tq[3];
   int restart = 0;
+  bool jfif = false, adobe = false;  // APP0 JFIF / APP14 Adobe seen (libjpeg's colour-space guess)
+  int adobe_transform = 0;
   const uint8_t* scan = nullptr;
   size_t scan_len = 0;
 };
@@ -121,6 +123,7 @@ int parse(const uint8_t* d, size_t len, Parsed& p, std::string& err) {
       f.width = (s[3] << 8) | s[4];
       f.ncomp = s[5];
       if (f.ncomp != 1 && f.ncomp != 3) return bad("1 or 3 components only");
+      if (have_sof) return bad("more than one frame header");
       if (sl < 6 + 3 * (size_t)f.ncomp || f.width <= 0 || f.height <= 0) return bad("SOF length");
       if ((long)f.width * f.height > (64L << 20)) return bad("image larger than 64 Mpixel");
       f.hmax = f.vmax = 1;
@@ -133,6 +136,10 @@ int parse(const uint8_t* d, size_t len, Parsed& p, std::string& err) {
         f.hmax = std::max(f.hmax, f.h[k]);
         f.vmax = std::max(f.vmax, f.v[k]);
       }
+      // one component = a non-interleaved scan (T.81 A.2.2): its MCU is one 8x8 block in raster
+      // order over ceil(W/8) x ceil(H/8), whatever sampling factors the SOF declares (libjpeg
+      // likewise walks a lone component's blocks with unit factors)
+      if (f.ncomp == 1) f.h[0] = f.v[0] = f.hmax = f.vmax = 1;
       have_sof = true;
     } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
       return bad("progressive / lossless / arithmetic JPEG");
@@ -149,10 +156,21 @@ int parse(const uint8_t* d, size_t len, Parsed& p, std::string& err) {
     } else if (m == 0xDD) {  // DRI
       if (sl < 2) return bad("DRI length");
       p.restart = (s[0] << 8) | s[1];
-    } else if (m == 0xEE && sl >= 12 && std::memcmp(s, "Adobe", 5) == 0 && s[11] != 1 && p.info.ncomp == 3) {
-      return bad("Adobe non-YCbCr transform");
+    } else if (m == 0xE0 && sl >= 5 && std::memcmp(s, "JFIF", 5) == 0) {  // APP0 JFIF
+      p.jfif = true;
+    } else if (m == 0xEE && sl >= 12 && std::memcmp(s, "Adobe", 5) == 0) {  // APP14 Adobe (any position)
+      p.adobe = true;
+      p.adobe_transform = s[11];
     } else if (m == 0xDA) {  // SOS
       if (!have_sof) return bad("SOS before SOF");
+      // colour space as libjpeg decides it (jdapimin.c default_decompress_parms) once every marker
+      // before the scan is known: JFIF -> YCbCr; else Adobe transform 0 -> RGB; else component ids
+      // 'R','G','B' -> RGB; else YCbCr.  Only YCbCr (or greyscale) is decoded here.
+      if (p.info.ncomp == 3 && !p.jfif) {
+        const bool rgb = p.adobe ? p.adobe_transform == 0
+                                 : (p.info.id[0] == 'R' && p.info.id[1] == 'G' && p.info.id[2] == 'B');
+        if (rgb) return bad("RGB-coded JPEG (no YCbCr transform)");
+      }
       const int ns = s[0];
       if (ns != p.info.ncomp) return bad("only single-scan interleaved JPEGs");
       for (int k = 0; k < ns; ++k) {
@@ -351,14 +369,21 @@ __device__ __forceinline__ uint32_t vcap_jpeg_range(long v) {
   return y < 128 ? (uint32_t)(y + 128) : y < 512 ? 255u : y < 896 ? 0u : (uint32_t)(y - 896);
 }
 
+// qt: this component's table of image 0; image i's is qt + i * qt_stride (frames of one clip may
+// carry different tables: ffmpeg's MJPEG rate control writes a per-frame qscale into each DQT).
 __global__ __launch_bounds__(256) void vcap_jpeg_idct_kernel(const int16_t* __restrict__ coef,
-                                                             const uint16_t* __restrict__ qt, uint8_t* __restrict__ plane,
-                                                             int bx, int by, long nblocks) {
+                                                             const uint16_t* __restrict__ qt, int qt_stride,
+                                                             uint8_t* __restrict__ plane, int bx, int by,
+                                                             long nblocks) {
   __shared__ int ws[32][8][9];  // [block][row][col] (+1 pad)
   const int t = threadIdx.x, lb = t >> 3, c = t & 7;
-  const long blk = (long)blockIdx.x * 32 + lb;
-  const bool live = blk < nblocks;
-  const int16_t* in = coef + (live ? blk : 0) * 64;
+  const long blk0 = (long)blockIdx.x * 32 + lb;
+  const bool live = blk0 < nblocks;
+  const long blk = live ? blk0 : 0;
+  const long per_img = (long)bx * by;
+  const long img = blk / per_img, rem = blk - img * per_img;
+  const int16_t* in = coef + blk * 64;
+  qt += img * qt_stride;
   // pass 1: column c, dequantised (the all-AC-zero shortcut is the same arithmetic)
   long d[8], r[8];
 #pragma unroll
@@ -375,8 +400,6 @@ __global__ __launch_bounds__(256) void vcap_jpeg_idct_kernel(const int16_t* __re
   uint32_t px[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) px[k] = vcap_jpeg_range((r[k] + (1L << (CB + P1 + 3 - 1))) >> (CB + P1 + 3));
-  const long per_img = (long)bx * by;
-  const long img = blk / per_img, rem = blk - img * per_img;
   const int byi = (int)(rem / bx), bxi = (int)(rem - (long)byi * bx);
   uint8_t* o = plane + img * per_img * 64 + ((long)(byi * 8 + c) * bx * 8) + bxi * 8;
   *reinterpret_cast<u32x2*>(o) =
@@ -467,7 +490,7 @@ static void jpeg_layout(const JpegInfo& f, int n, size_t* comp_off, size_t* coef
 size_t vcap_jpeg_ws_bytes(const JpegInfo& f, int n) {
   size_t co[3], ce, po[3], pb;
   jpeg_layout(f, n, co, &ce, po, &pb);
-  return ((ce * sizeof(int16_t) + 255) & ~(size_t)255) + pb + 4 * 64 * sizeof(uint16_t) + 256;
+  return ((ce * sizeof(int16_t) + 255) & ~(size_t)255) + pb + (size_t)n * 3 * 64 * sizeof(uint16_t) + 256;
 }
 
 int vcap_jpeg_decode(const uint8_t* const* data, const size_t* lens, int n, uint8_t* out, void* ws, size_t ws_bytes,
@@ -483,9 +506,8 @@ int vcap_jpeg_decode(const uint8_t* const* data, const size_t* lens, int n, uint
     const JpegInfo &a = ps[0].info, &b = ps[i].info;
     bool same = a.width == b.width && a.height == b.height && a.ncomp == b.ncomp;
     for (int k = 0; same && k < a.ncomp; ++k) same = a.h[k] == b.h[k] && a.v[k] == b.v[k];
-    for (int k = 0; same && k < a.ncomp; ++k) same = std::memcmp(ps[0].qt[ps[0].tq[k]], ps[i].qt[ps[i].tq[k]], 128) == 0;
     if (!same) {
-      *err = "image " + std::to_string(i) + ": size, sampling or quantisation tables differ from image 0";
+      *err = "image " + std::to_string(i) + ": size or chroma sampling differs from image 0";
       return VCAP_E_UNSUPPORTED;
     }
   }
@@ -504,11 +526,12 @@ int vcap_jpeg_decode(const uint8_t* const* data, const size_t* lens, int n, uint
   // buffer (kept for the process: pageable memory halved the upload rate of the coefficients,
   // which are n x 128 B per 8x8 block)
   std::lock_guard<std::mutex> lock(g_stage_mu);
-  if (g_stage_bytes < coef_elems * sizeof(int16_t)) {
+  const size_t stage_need = ((coef_elems * sizeof(int16_t) + 15) & ~(size_t)15) + (size_t)n * 3 * 64 * sizeof(uint16_t);
+  if (g_stage_bytes < stage_need) {
     if (g_stage) (void)hipHostFree(g_stage);
     g_stage = nullptr;
     g_stage_bytes = 0;
-    const size_t want = coef_elems * sizeof(int16_t) + (coef_elems * sizeof(int16_t)) / 4;
+    const size_t want = stage_need + stage_need / 4;
     if (hipHostMalloc(&g_stage, want, hipHostMallocDefault) != hipSuccess) {
       g_stage = nullptr;
       *err = "jpeg decode: pinned staging allocation failed";
@@ -529,14 +552,20 @@ int vcap_jpeg_decode(const uint8_t* const* data, const size_t* lens, int n, uint
   int16_t* d_coef = (int16_t*)w;
   uint8_t* d_planes = (uint8_t*)(w + ((coef_elems * sizeof(int16_t) + 255) & ~(size_t)255));
   uint16_t* d_qt = (uint16_t*)(d_planes + plane_bytes);
-  uint16_t qts[3][64];
-  for (int k = 0; k < f.ncomp; ++k) std::memcpy(qts[k], ps[0].qt[ps[0].tq[k]], sizeof(qts[k]));
+  // every image's own tables, [image][component][64] natural order, staged behind the coefficients
+  uint16_t* qts = (uint16_t*)((char*)g_stage + ((coef_elems * sizeof(int16_t) + 15) & ~(size_t)15));
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < f.ncomp; ++k) std::memcpy(qts + ((size_t)i * f.ncomp + k) * 64, ps[i].qt[ps[i].tq[k]], 128);
   hipError_t he = hipMemcpyAsync(d_coef, coef, coef_elems * sizeof(int16_t), hipMemcpyHostToDevice, s);
-  if (he == hipSuccess) he = hipMemcpyAsync(d_qt, qts, sizeof(uint16_t) * 64 * f.ncomp, hipMemcpyHostToDevice, s);
+  // from here on the pinned staging buffer may be read by an in-flight copy: every return below
+  // synchronises the stream first (the next call reuses or frees the buffer)
+  const bool enqueued = he == hipSuccess;
+  if (he == hipSuccess)
+    he = hipMemcpyAsync(d_qt, qts, sizeof(uint16_t) * 64 * f.ncomp * (size_t)n, hipMemcpyHostToDevice, s);
   for (int k = 0; k < f.ncomp && he == hipSuccess; ++k) {
     const long nb = (long)n * f.bx[k] * f.by[k];
     hipLaunchKernelGGL(vcap_jpeg_idct_kernel, dim3((unsigned)((nb + 31) / 32)), dim3(256), 0, s, d_coef + comp_off[k],
-                       d_qt + 64 * k, d_planes + plane_off[k], f.bx[k], f.by[k], nb);
+                       d_qt + 64 * k, 64 * f.ncomp, d_planes + plane_off[k], f.bx[k], f.by[k], nb);
     he = hipGetLastError();
   }
   if (he == hipSuccess) {
@@ -555,8 +584,11 @@ int vcap_jpeg_decode(const uint8_t* const* data, const size_t* lens, int n, uint
                        f.width, f.height, total, out);
     he = hipGetLastError();
   }
-  // the staging buffer is reused by the next call: the copy must have finished
-  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  // the staging buffer is reused by the next call: the copies must have finished, on every path
+  if (enqueued) {
+    const hipError_t hs = hipStreamSynchronize(s);
+    if (he == hipSuccess) he = hs;
+  }
   if (he != hipSuccess) {
     *err = std::string("jpeg decode: ") + hipGetErrorString(he);
     return -(int)he;

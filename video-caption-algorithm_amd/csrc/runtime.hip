@@ -175,6 +175,7 @@ struct DecBufs {
   int* finished;
   float* proc;        // [B][V] processed scores (sampling mode)
   unsigned* seed;     // [2] Philox key of the sampling draws
+  unsigned* persist;  // persistent decode: barrier words + device layer table
 };
 
 int max_logit_blocks(int V, int B) { return vcap_logit_blocks(V, B); }
@@ -196,7 +197,8 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.kc = c.take(per_layer * d->n_layer * es);
   b.vc = c.take(per_layer * d->n_layer * es);
   b.pt = (int*)c.take(pages * 4);
-  const int nb = max_logit_blocks(d->vocab, B);
+  // argmax partials: the launch chain's lm_head blocks, or the persistent decode's <= 256 workgroups
+  const int nb = std::max(max_logit_blocks(d->vocab, B), 256);
   b.pval = (float*)c.take((size_t)B * nb * 4);
   b.pidx = (int*)c.take((size_t)B * nb * 4);
   b.hist = (int*)c.take((size_t)B * max_new * 4);
@@ -205,6 +207,7 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.finished = (int*)c.take((size_t)B * 4);
   b.proc = (float*)c.take((size_t)B * d->vocab * 4);
   b.seed = (unsigned*)c.take(8);
+  b.persist = (unsigned*)c.take(vcap_persist_ws_bytes());
   return b;
 }
 
@@ -298,6 +301,27 @@ int run_lm_head(const vcap_gpt2_desc* d, const DecBufs& w, int rows, int S_new, 
   return 0;
 }
 
+// Workgroups of the persistent decode for this call, 0 = the launch chain.  gp->persistent: 0 off,
+// > 0 that many workgroups, < 0 auto (VCAP_PERSIST_G or 128).  Eligible: bf16, <= 16 rows, greedy
+// (no sampling), GPT-2 widths the kernel is instantiated for, at most one workgroup per CU.
+int persist_wgs(const vcap_gpt2_desc* d, const vcap_gen_params* gp, int B, int max_new, bool sampling) {
+  if (gp->persistent == 0 || sampling || d->dtype != VCAP_DT_BF16 || B > 16 || max_new < 2) return 0;
+  if (d->n_embd != 768 && d->n_embd != 1024 && d->n_embd != 128) return 0;
+  if (d->n_layer > kPersistMaxLayers) return 0;
+  int G = gp->persistent;
+  if (G < 0) {
+    static const int env = [] {
+      const char* e = std::getenv("VCAP_PERSIST_G");
+      return e ? (int)std::strtol(e, nullptr, 10) : 0;
+    }();
+    G = env > 0 ? env : 128;
+  }
+  G = std::max(G, vcap_persist_min_wgs(d->n_embd));
+  if (G > vcap_device_cus() || G > 256) return 0;
+  if ((d->vocab + 15) / 16 > 64 * G || B * d->n_head > 4 * G) return 0;
+  return G;
+}
+
 // sp != nullptr: sampling mode (HF _sample): the lm_head also stores the processed scores, the
 // sample kernel warps them and draws (or takes force_ids), and hands the token to the finalize kernel
 int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* ids, int nids,
@@ -309,7 +333,26 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
   const int dt = d->dtype;
   VCAP_TRY(vcap_decode_init_dispatch(w.pt, B, maxp, w.finished, w.nbanned, s), "decode_init");
   VCAP_TRY(vcap_prefill_embed_dispatch(dt, prefix, P, ids, nids, d->wte, d->wpe, w.h, B, E, s), "prefill_embed");
+  const int G = persist_wgs(d, gp, B, max_new, sp != nullptr);
   for (int step = 0; step < max_new; ++step) {
+    if (G > 0 && step == 1) {
+      // steps 1 .. max_new-1: one persistent launch (csrc/decode_persist.hip), bit-identical
+      PersistDesc pd;
+      memset(&pd, 0, sizeof(pd));
+      pd.G = G; pd.M = B; pd.E = E; pd.H = d->n_head; pd.L = d->n_layer; pd.V = V; pd.S0 = S0; pd.maxp = maxp;
+      pd.n_pos = d->n_positions; pd.step0 = 1; pd.step1 = max_new; pd.ln_eps = d->ln_eps;
+      pd.lnf_g = d->lnf_g; pd.lnf_b = d->lnf_b; pd.lm_head = d->lm_head; pd.wte = d->wte; pd.wpe = d->wpe;
+      pd.h = w.h; pd.q = w.q; pd.attn = w.attn; pd.act = w.act; pd.kc = w.kc; pd.vc = w.vc;
+      pd.page_elems = (long)page_elems;
+      pd.hist = w.hist; pd.banned = w.banned; pd.nbanned = w.nbanned; pd.finished = w.finished;
+      pd.hist_ld = max_new; pd.ngram = gp->no_repeat_ngram_size; pd.rep = gp->repetition_penalty;
+      pd.min_new = gp->min_new_tokens; pd.eos = gp->eos_token_id; pd.pad = gp->pad_token_id;
+      pd.out_ids = out_ids; pd.out_ld = max_new; pd.logits_out = logits_out;
+      pd.pval = w.pval; pd.pidx = w.pidx; pd.bar = w.persist;
+      pd.layers = reinterpret_cast<const PersistLayer*>(d->layers);
+      VCAP_TRY(vcap_decode_persist_dispatch(pd, s), "decode_persist");
+      break;
+    }
     const int S_new = step == 0 ? S0 : 1;
     const int past = step == 0 ? 0 : S0 + step - 1;
     if (int rc = run_layers(d, w, maxp, page_elems, B * S_new, S_new, past, gp->max_blocks, s)) return rc;
@@ -320,7 +363,8 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
       return rc;
     if (sp) {
       SampleArgs sa{w.proc, V, V, sp->temperature, sp->top_k, sp->top_p, w.seed, step, force_ids, max_new,
-                    warped_out ? warped_out + (size_t)step * B * V : nullptr, V, w.pval, w.pidx};
+                    warped_out ? warped_out + (size_t)step * B * V : nullptr, V, w.pval, w.pidx,
+                    gp->eos_token_id};
       VCAP_TRY(vcap_sample_dispatch(sa, B, s), "sample");
       nblk = 1;
     }
@@ -1143,6 +1187,8 @@ int vcap_decode_attention(int dtype, const void* q, const void* k_pool, const vo
            "vcap_decode_attention");
   return 0;
 }
+
+unsigned vcap_decode_faults(void) { return vcap_decode_persist_faults(); }
 
 void vcap_graph_cache_clear(void) {
   std::vector<GraphEntry> evicted;

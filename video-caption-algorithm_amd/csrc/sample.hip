@@ -108,7 +108,12 @@ __global__ __launch_bounds__(kThreads) void vcap_sample_kernel(SampleArgs a) {
     o_idx[r] = xi;
   }
   __syncthreads();
-  if (t == 0) {
+  if (t == 0 && nc == 0) {
+    // no finite processed score in the row (NaN or all -inf logits): a defined token, no draw
+    s_nc = 0;
+    a.pval[row] = 0.f;
+    a.pidx[row] = a.force ? min(max(a.force[(long)row * a.force_ld + a.step], 0), V - 1) : a.eos;
+  } else if (t == 0) {
     // ---- TopP over the survivors (every other score is -inf: probability 0)
     const float mx = o_val[nc - 1];
     float sum = 0.f;
@@ -143,7 +148,7 @@ __global__ __launch_bounds__(kThreads) void vcap_sample_kernel(SampleArgs a) {
         break;
       }
     }
-    if (a.force) tok = a.force[(long)row * a.force_ld + a.step];
+    if (a.force) tok = min(max(a.force[(long)row * a.force_ld + a.step], 0), V - 1);  // finalize indexes wte
     s_tok = tok;
     s_nc = j0;  // reused: first kept survivor
     a.pval[row] = 0.f;

@@ -76,6 +76,7 @@ struct SampleArgs {
   long warped_ld;
   float* pval;           // [rows]: the token as the finalize kernel's only argmax partial
   int* pidx;
+  int eos;               // emitted for a row with no finite processed score (NaN / all -inf logits)
 };
 hipError_t vcap_sample_dispatch(const SampleArgs& a, int rows, hipStream_t s);
 int vcap_sample_max_top_k();
@@ -158,6 +159,61 @@ int vcap_beam_chunks(int V);
 hipError_t vcap_decode_attention_anc_dispatch(int dt, const void* q, const void* kc, const void* vc, const int* anc,
                                               int anc_ld, int maxp, void* out, int M, int H, int past,
                                               hipStream_t s);
+
+// ---- persistent greedy decode (csrc/decode_persist.hip): steps [step0, step1) of a bf16 decode of
+// M <= 16 rows as one launch of G workgroups (one per CU); state as the launch chain leaves it
+constexpr int kPersistMaxLayers = 24;
+struct PersistLayer {  // same field order as vcap_gpt2_layer (include/vcap.h)
+  const float* ln1_g;
+  const float* ln1_b;
+  const void* attn_w;
+  const float* attn_b;
+  const void* aproj_w;
+  const float* aproj_b;
+  const float* ln2_g;
+  const float* ln2_b;
+  const void* fc_w;
+  const float* fc_b;
+  const void* mproj_w;
+  const float* mproj_b;
+};
+struct PersistDesc {
+  int G, M, E, H, L, V, S0, maxp, n_pos;
+  int step0, step1;
+  float ln_eps;
+  const float* lnf_g;
+  const float* lnf_b;
+  const void* lm_head;
+  const void* wte;
+  const float* wpe;
+  float* h;
+  void* q;
+  void* attn;
+  void* act;
+  void* kc;
+  void* vc;
+  long page_elems;
+  int* hist;
+  int* banned;
+  int* nbanned;
+  int* finished;
+  int hist_ld;
+  int ngram;
+  float rep;
+  int min_new, eos, pad;
+  int* out_ids;
+  int out_ld;
+  float* logits_out;   // optional [hist_ld][M][V] (row block of step s at s * M * V)
+  float* pval;         // [M][G]
+  int* pidx;
+  unsigned* bar;       // vcap_persist_ws_bytes(): arrival counters (zeroed by the dispatch) + layer table
+  const PersistLayer* layers;
+};
+hipError_t vcap_decode_persist_dispatch(const PersistDesc& d, hipStream_t s);
+int vcap_persist_min_wgs(int E);
+size_t vcap_persist_bar_bytes();
+size_t vcap_persist_ws_bytes();   // at d.bar: barrier words, then the device layer table
+unsigned vcap_decode_persist_faults();
 
 hipError_t vcap_kv_gather_dispatch(int dt, const void* src_pool, void* dst_pool, const int* src_rows, int rows, int maxp,
                                    int H, int len, long layer_elems, int L, hipStream_t s);

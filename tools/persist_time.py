@@ -2,6 +2,7 @@
 at several grid sizes.  step = (t[24-token graph] - t[2-token graph]) / 22, both replayed after
 warm-up (the prefill and step 0 cancel).  usage: python tools/persist_time.py [B ...]"""
 import dataclasses
+import os
 import sys
 import time
 from pathlib import Path
@@ -42,7 +43,8 @@ def main():
                                   .astype(np.float32)).to(dev)
         base = GenConfig(24, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, True)
         ref = None
-        for G in (0, 96, 128, 160, 192, 256):
+        gs = os.environ.get("PERSIST_GS")
+        for G in ([int(x) for x in gs.split(",")] if gs else (0, 96, 128, 160, 192, 256)):
             t24, ids = replay_s(dec, prefix, dataclasses.replace(base, persistent=G), ga)
             t2, _ = replay_s(dec, prefix, dataclasses.replace(base, max_new_tokens=2, persistent=G), ga)
             ref = ids if ref is None else ref

@@ -12,9 +12,19 @@ from collections import defaultdict
 out_dir, token_steps, dst = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 vit_rows = int(sys.argv[4]) if len(sys.argv) > 4 else 25216
 acc = defaultdict(lambda: defaultdict(list))
+# attn-proj and fc2 run the same kernel (gemm256<bf16, f32, 2>, in-place f32 residual) on the same
+# grid; in every pass they are dispatched alternately (per layer: attn-proj, then fc2), so their
+# records are split by dispatch order into "...[attn-proj]" / "...[fc2]"
+RESID = "vcap_gemm256_kernel<unsigned short, float, 2>"
 for f in glob.glob(f"{out_dir}/*/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        acc[r.get("Kernel_Name", "")][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    rows = list(csv.DictReader(open(f)))
+    resid_ids = sorted({int(r.get("Dispatch_Id", 0)) for r in rows if RESID in r.get("Kernel_Name", "")})
+    role = {d: ("[attn-proj]" if i % 2 == 0 else "[fc2]") for i, d in enumerate(resid_ids)}
+    for r in rows:
+        name = r.get("Kernel_Name", "")
+        if RESID in name:
+            name = name.split("(")[0] + role[int(r.get("Dispatch_Id", 0))]
+        acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 
 
 def avg(v):
@@ -24,7 +34,7 @@ def avg(v):
 kernels = {}
 dec_bytes = 0.0
 for name, c in acc.items():
-    short = name.split("(")[0].replace("void ", "")
+    short = (name if name.endswith("]") else name.split("(")[0]).replace("void ", "")
     fetch, write = avg(c.get("FETCH_SIZE", [])), avg(c.get("WRITE_SIZE", []))
     grbm, mfma = avg(c.get("GRBM_GUI_ACTIVE", [])), avg(c.get("SQ_VALU_MFMA_BUSY_CYCLES", []))
     k = {"launches": len(c.get("GRBM_GUI_ACTIVE", [])),

@@ -44,6 +44,7 @@ __device__ __forceinline__ u32x4 vcap_dec_aload(const void* base, long off_bytes
 #include "vcap_kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 // ------------------------------------------------------------------------------------------------
 // Weight packing (one-time, at model load).
@@ -867,6 +868,206 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
   return launch_generic<T, MT, NTB, PRO, EPI>(a, s);
 }
 
+// ------------------------------------------------------------------------------------------------
+// lm_head (PRO_LN + EPI_LOGITS) at M <= 16 rows as a weight stream: one workgroup per CU walks a
+// contiguous range of `tpw` 16-column tiles (ln_f computed once per workgroup instead of once per 4
+// tiles), NTB tiles per group with the next group's weight fragments issued before this group's
+// MFMAs (two register sets), the processors applied per element and a running argmax per row; one
+// (max, index) partial per row per workgroup (nblk = grid).  The 77 MB of a GPT-2 vocab then
+// streams on ~250 workgroups that all finish together instead of 786 workgroups at 2 per CU, whose
+// last ~third ran after the rest (profiles/r03_decode_stamps.txt: 21 us per step, 14 us of it skew).
+// Per-element arithmetic (K split over the 4 waves, MFMA order, (w0 + w1) + (w2 + w3) reduction,
+// processors) is that of vcap_rows_gemv_kernel, so logits and ids are bit-identical; the argmax is
+// a total order (value, then lowest index), so its grouping does not matter.
+template <typename T, int NSL, int NTB>
+__global__ __launch_bounds__(256) void vcap_lm_head_stream_kernel(RowsGemmArgs a, int tpw) {
+  extern __shared__ __attribute__((aligned(16))) char dyn[];  // A tile [16][K] T, then flags
+  constexpr int E8 = Frag<T>::kElems, KS = 4 * E8, K = 4 * NSL * KS;
+  constexpr int KC = (K + 255) / 256;
+  constexpr int kMaxCols = 32 * 16;  // tpw <= 32
+  __shared__ __attribute__((aligned(16))) float red[4][NTB * 256];
+  unsigned char* s_rep = reinterpret_cast<unsigned char*>(dyn + 16 * K * sizeof(T));
+  unsigned char* s_ban = s_rep + 16 * kMaxCols;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int M = a.M, N = a.N;
+  const int nslab = 4 * NSL, g0 = wave * NSL;
+  const int ntiles = (N + 15) >> 4;
+  const int t0 = blockIdx.x * tpw, t1 = min(t0 + tpw, ntiles);
+  const int c_begin = t0 * 16, ncols = (t1 - t0) * 16;
+  const int ngr = (t1 - t0 + NTB - 1) / NTB;
+  auto issue = [&](u32x4 (&wf)[NSL][NTB], int gi) {
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) {
+      const u32x4* wp = packed_frag(a.w, min(t0 + gi * NTB + j, t1 - 1), nslab, g0, lane);
+#pragma unroll
+      for (int s = 0; s < NSL; ++s) wf[s][j] = vcap_dec_wload<true>(a.w, wp + s * 64);
+    }
+  };
+  // first group's weights + ln_f rows + processor token lists, all issued up front
+  u32x4 wA[NSL][NTB], wB[NSL][NTB];
+  f32x4 xv[4][KC], gv[KC], bv[KC];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const long xo = (long)min(wave + 4 * r, M - 1) * a.ldx;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      xv[r][c] = __builtin_bit_cast(f32x4, vcap_dec_aload(a.x, (xo + min(c * 256 + lane * 4, K - 4)) * 4L));
+  }
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    gv[c] = *reinterpret_cast<const f32x4*>(a.ln_g + min(c * 256 + lane * 4, K - 4));
+    bv[c] = *reinterpret_cast<const f32x4*>(a.ln_b + min(c * 256 + lane * 4, K - 4));
+  }
+  issue(wA, 0);
+  int htk[4], btk[4], nbk[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = tid + q * 256, m = min(i >> 6, M - 1), t = min(i & 63, a.hist_ld - 1);
+    htk[q] = a.hist[m * a.hist_ld + t];
+    btk[q] = a.banned[m * a.hist_ld + t];
+    nbk[q] = a.nbanned[m];
+  }
+  for (int i = tid; i < 2 * 16 * kMaxCols / 4; i += 256) reinterpret_cast<unsigned*>(s_rep)[i] = 0u;
+  // ln_f (vcap_rows_gemv_kernel PRO_LN arithmetic; the clamped chunks past K do not contribute)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = wave + 4 * r;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      if (c * 256 + lane * 4 < K) s += (xv[r][c].x + xv[r][c].y) + (xv[r][c].z + xv[r][c].w);
+    const float mean = wave_sum(s) / (float)K;
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      if (c * 256 + lane * 4 < K) {
+        const f32x4 d = xv[r][c] - mean;
+        ss += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+      }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)K + a.ln_eps);
+    const bool live = m < M;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      if (c * 256 + lane * 4 < K) {
+        const f32x4 y = live ? (xv[r][c] - mean) * rstd * gv[c] + bv[c] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        const int byte = (c * 256 + lane * 4) * (int)sizeof(T);
+        char* dst = dyn + (long)m * (K * (int)sizeof(T)) + ((((byte >> 4) ^ (m & 15))) << 4) + (byte & 15);
+        if constexpr (sizeof(T) == 2) {
+          *reinterpret_cast<u32x2*>(dst) = (u32x2){pack_bf2(y.x, y.y), pack_bf2(y.z, y.w)};
+        } else {
+          *reinterpret_cast<f32x4*>(dst) = y;
+        }
+      }
+    }
+  }
+  __syncthreads();  // flags zeroed, A tile written
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = tid + q * 256, m = i >> 6, t = i & 63;
+    if (m >= M) continue;
+    const unsigned hc = (unsigned)(htk[q] - c_begin), bc = (unsigned)(btk[q] - c_begin);
+    if (a.rep_penalty != 1.0f && t < a.gen_len && hc < (unsigned)ncols) s_rep[m * kMaxCols + hc] = 1;
+    if (t < nbk[q] && bc < (unsigned)ncols) s_ban[m * kMaxCols + bc] = 1;
+  }
+  __syncthreads();
+  const int row = tid >> 4, col = tid & 15;
+  float bv_run = -INFINITY;
+  int bi_run = 0x7fffffff;
+  auto group = [&](const u32x4 (&wf)[NSL][NTB], int gi) {
+    f32x4 acc[NTB];
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+      const int chunk = (g0 + s) * 4 + fg;
+      const u32x4 A = *reinterpret_cast<const u32x4*>(dyn + (long)fr * K * sizeof(T) + ((chunk ^ fr) << 4));
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) acc[j] = mfma_frag(A, wf[s][j], acc[j], (T*)nullptr);
+    }
+#pragma unroll
+    for (int j = 0; j < NTB; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][j * 256 + (fg * 4 + r) * 16 + fr] = acc[j][r];
+    __syncthreads();
+    if (row < M) {
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) {
+        const int t = t0 + gi * NTB + j, n = t * 16 + col;
+        if (t < t1 && n < N) {
+          const int e = j * 256 + row * 16 + col;
+          const float v = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]) + 0.f;
+          if (a.logits_raw) a.logits_raw[(long)row * N + n] = v;
+          float sv = v;
+          const int li = row * kMaxCols + (n - c_begin);
+          if (s_rep[li]) sv = sv < 0.f ? sv * a.rep_penalty : sv / a.rep_penalty;
+          if (s_ban[li]) sv = -INFINITY;
+          if (n == a.eos && a.gen_len < a.min_new) sv = -INFINITY;
+          if (a.proc_out) a.proc_out[(long)row * N + n] = sv;
+          argmax_take(bv_run, bi_run, sv, n);
+        }
+      }
+    }
+    __syncthreads();
+  };
+  for (int gi = 0; gi < ngr; gi += 2) {
+    if (gi + 1 < ngr) issue(wB, gi + 1);
+    group(wA, gi);
+    if (gi + 1 < ngr) {
+      if (gi + 2 < ngr) issue(wA, gi + 2);
+      group(wB, gi + 1);
+    }
+  }
+  argmax_take(bv_run, bi_run, dpp_f<DPP_XOR1>(bv_run), dpp_i<DPP_XOR1>(bi_run));
+  argmax_take(bv_run, bi_run, dpp_f<DPP_XOR2>(bv_run), dpp_i<DPP_XOR2>(bi_run));
+  argmax_take(bv_run, bi_run, dpp_f<DPP_HALF_MIRROR>(bv_run), dpp_i<DPP_HALF_MIRROR>(bi_run));
+  argmax_take(bv_run, bi_run, dpp_f<DPP_MIRROR>(bv_run), dpp_i<DPP_MIRROR>(bi_run));
+  if (col == 0 && row < M) {
+    a.part_val[(long)row * gridDim.x + blockIdx.x] = bv_run;
+    a.part_idx[(long)row * gridDim.x + blockIdx.x] = bi_run;
+  }
+}
+
+template <typename T, int NSL>
+static hipError_t launch_lm_stream(const RowsGemmArgs& a, int* nblk_out, hipStream_t s) {
+  constexpr int NTB = (NSL <= 8) ? 4 : 2;  // two register sets of NSL x NTB fragments
+  const int ntiles = (a.N + 15) / 16;
+  const int cus = vcap_device_cus();
+  int tpw = (ntiles + cus - 1) / cus;
+  if (tpw > 32) return hipErrorInvalidValue;
+  const int grid = (ntiles + tpw - 1) / tpw;
+  const size_t lds = (size_t)16 * (4 * NSL * 4 * Frag<T>::kElems) * sizeof(T) + 2 * 16 * 32 * 16;
+  static int limit = 0;
+  if ((size_t)allow_lds(vcap_lm_head_stream_kernel<T, NSL, NTB>, limit) < lds) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((vcap_lm_head_stream_kernel<T, NSL, NTB>), dim3(grid), dim3(256), lds, s, a, tpw);
+  if (nblk_out) *nblk_out = grid;
+  return hipGetLastError();
+}
+
+// M <= 16 lm_head as the weight stream above (VCAP_LM_STREAM=0 keeps the 64-column GEMV blocks);
+// returns false where it does not apply
+static bool try_lm_stream(int dt, const RowsGemmArgs& a, int* nblk_out, hipStream_t s, hipError_t& err) {
+  static const bool on = [] {
+    const char* e = std::getenv("VCAP_LM_STREAM");
+    return !e || std::strtol(e, nullptr, 10) != 0;
+  }();
+  if (!on || a.M > 16 || a.hist_ld > 64) return false;
+  const int nsl = a.K / (16 * (dt == VCAP_DT_BF16 ? 8 : 4));
+  if ((long)a.M * a.ldx * 4 >= 0x7FFFFFFFL) return false;
+#define VCAP_LMS(TT, NN) \
+  if (nsl == NN) {       \
+    err = launch_lm_stream<TT, NN>(a, nblk_out, s); \
+    return true;         \
+  }
+  if (dt == VCAP_DT_BF16) {
+    VCAP_LMS(bf16_t, 1) VCAP_LMS(bf16_t, 6) VCAP_LMS(bf16_t, 8)
+  } else {
+    VCAP_LMS(float, 2) VCAP_LMS(float, 12) VCAP_LMS(float, 16)
+  }
+#undef VCAP_LMS
+  return false;
+}
+
 // 16-column tiles per workgroup: the lm_head always takes 4 (argmax partials per 64 columns; 786
 // workgroups at 2 per CU.  r03: 2, 5 or 8 tiles per workgroup (1571 / 629 / 393 workgroups) measured
 // +1-2 / +6 / +8 us per token step, and forcing 3 workgroups per CU (<= 168 VGPRs) +22 us);
@@ -890,6 +1091,10 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
   if (a.K % ks4 != 0 || a.M <= 0 || a.K <= 0 || a.N <= 0) return hipErrorInvalidValue;
   if (pro == PRO_LN && a.K > 1024) return hipErrorInvalidValue;
   if (epi == EPI_LOGITS && a.hist_ld > 64) return hipErrorInvalidValue;
+  if (pro == PRO_LN && epi == EPI_LOGITS) {
+    hipError_t err = hipSuccess;
+    if (try_lm_stream(dt, a, nblk_out, s, err)) return err;
+  }
   const int ntb = rows_ntb(epi, a.N, a.max_blocks);
   if (nblk_out) *nblk_out = (a.N + ntb * 16 - 1) / (ntb * 16);
   const bool one = a.M <= 16;
@@ -950,7 +1155,7 @@ __global__ __launch_bounds__(256) void vcap_decode_attention_c64_kernel(const bf
   __shared__ float s_q[4][64];
   __shared__ float s_p[4][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int item = blockIdx.x * 4 + wave;
+  const int item = blockIdx.x * (int)(blockDim.x >> 6) + wave;  // one wave per item
   if (item >= M * H) return;
   const int m = item / H, h = item - m * H;
   const int E = H * 64;
@@ -1015,8 +1220,16 @@ hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc,
   if (past + S_new > 1024 || maxp > 64) return hipErrorInvalidValue;
   const dim3 grid((M * H + 3) / 4), block(256);
   if (dt == VCAP_DT_BF16 && !pt && past + S_new <= 64) {
-    hipLaunchKernelGGL(vcap_decode_attention_c64_kernel, grid, block, 0, s, (const bf16_t*)q, (const bf16_t*)kc,
-                       (const bf16_t*)vc, maxp, (bf16_t*)out, M, H, S_new, past);
+    // one 64-thread workgroup per (row, head): the ~100-200 items of a decode step spread over as
+    // many CUs (each item's q / K / V round trip on a CU of its own) instead of 4 per CU
+    static const int per_wg = [] {
+      const char* e = std::getenv("VCAP_ATTN_WAVES");
+      const int v = e ? (int)std::strtol(e, nullptr, 10) : 1;
+      return v >= 1 && v <= 4 ? v : 1;
+    }();
+    hipLaunchKernelGGL(vcap_decode_attention_c64_kernel, dim3((M * H + per_wg - 1) / per_wg), dim3(64 * per_wg), 0,
+                       s, (const bf16_t*)q, (const bf16_t*)kc, (const bf16_t*)vc, maxp, (bf16_t*)out, M, H, S_new,
+                       past);
     return hipGetLastError();
   }
   if (!pt) return hipErrorInvalidValue;  // the general kernels read the page table

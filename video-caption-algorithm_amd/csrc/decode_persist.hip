@@ -55,6 +55,10 @@ constexpr int kShardStride = 32;                 // words between counter shards
 constexpr int kAbortWord = 8 * kShardStride;
 
 __device__ unsigned g_persist_faults;
+// diagnostic (VCAP_PERSIST_FLAGS & 8): s_memrealtime at each phase's arrival and release, per
+// workgroup: [wg][phase][2] (tools/persist_time.py --stamps)
+constexpr int kStampPhases = 2048;
+__device__ unsigned long g_persist_stamps[256][kStampPhases][2];
 
 // Every handed-off buffer lives in the decoder workspace and is addressed as a byte offset from its
 // base through ONE buffer resource (4 SGPRs: a resource per buffer held ~40 SGPRs live across the
@@ -331,7 +335,10 @@ VCAP_DEV void attn_item(const PersistArgs& a, int okc, int ovc, int m, int h, in
 //   s_h [1024] int (P7) | scalars
 template <int E>
 struct Lds {
-  static constexpr int kRed = 0;
+  // the barrier flag and scalars live OUTSIDE the region P5's weight DMA lands in: that DMA is in
+  // flight across the P4 -> P5 barrier, which writes the flag
+  static constexpr int kMisc = 0;
+  static constexpr int kRed = 128;
   static constexpr int kW5 = kRed + 4 * 4 * 256 * 4;   // P5's weights (LDS-DMA), overlapping the rest
   static constexpr int kA = kW5;
   static constexpr int kSq = kA + 16 * E * 2;
@@ -339,10 +346,9 @@ struct Lds {
   static constexpr int kRep = kSp + 4 * 1024 * 4;
   static constexpr int kBan = kRep + 16 * kTpw * 16;
   static constexpr int kHist = kBan + 16 * kTpw * 16;
-  static constexpr int kMisc = kHist + 1024 * 4;
   // > 80 KiB: one workgroup per CU (the grid's co-residency then needs G CUs, and each workgroup's
   // weight stream has a CU's load path to itself)
-  static constexpr int kEnd = kMisc + 128 > kW5 + 4 * (E / 32) * 1024 ? kMisc + 128 : kW5 + 4 * (E / 32) * 1024;
+  static constexpr int kEnd = kHist + 4096 > kW5 + 4 * (E / 32) * 1024 ? kHist + 4096 : kW5 + 4 * (E / 32) * 1024;
   static constexpr int kBytes = kEnd > 82 * 1024 ? kEnd : 82 * 1024;
   static_assert(kBytes <= 160 * 1024, "LDS per CU");
 };
@@ -386,11 +392,21 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
   auto drain = [&]() {
     if (threadIdx.x < kCompute) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
+  // raw s_barrier + lgkmcnt(0) (LDS only): __syncthreads() would also wait vmcnt(0), i.e. for the
+  // next phase's weights just issued (P5's LDS-DMA counts as a pending LDS write) - the very latency
+  // the prefetch is there to hide behind the grid barrier
+  auto wg_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
   auto barrier = [&]() -> bool {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    __syncthreads();
+    wg_barrier();
     ++phase;
     if (wave == 4) {
+      if ((a.flags & 8) && lane == 0 && phase <= kStampPhases)
+        g_persist_stamps[blockIdx.x][phase - 1][0] = __builtin_amdgcn_s_memrealtime();
       if (lane == 0)
         __hip_atomic_fetch_add(a.bar + (blockIdx.x & 7) * kShardStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned target = phase * (unsigned)G;
@@ -419,8 +435,10 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
         if (!(a.flags & 4)) __builtin_amdgcn_s_sleep(1);
       }
       if (lane == 0) s_misc[0] = ok;
+      if ((a.flags & 8) && lane == 0 && phase <= kStampPhases)
+        g_persist_stamps[blockIdx.x][phase - 1][1] = __builtin_amdgcn_s_memrealtime();
     }
-    __syncthreads();
+    wg_barrier();
     return s_misc[0] != 0;
   };
 
@@ -447,13 +465,13 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
         VCAP_PHASE_IDS();
         const bool act = wg < nt_qkv;
         if (compute && act) ln_rows<E>(a.base, a.o_h, M, ly.ln1_g, ly.ln1_b, a.ln_eps, dyn, wave, lane);
-        __syncthreads();
+        wg_barrier();
         if (compute && act) {
           f32x4 acc[2];
           mma_lds<E, NSL1, 2>(acc, wq, dyn, wave, lane);
           to_red<2>(red, acc, wave, lane);
         }
-        __syncthreads();
+        wg_barrier();
         if (compute && act) {
           const int j = tid >> 7, row = (tid >> 3) & 15, c0 = (tid & 7) * 2;
           const int t = wg + j * G;
@@ -505,7 +523,7 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
           for (int s = 0; s < NSL1; ++s) acc[0] = mfma_frag(af[s], wq[s], acc[0], (bf16_t*)nullptr);
           to_red<1>(red, acc, wave, lane);
         }
-        __syncthreads();
+        wg_barrier();
         if (compute && act && tid < 128 && row < M) {
           const float v0 = __uint_as_float(res.x) + red_val(red, 0, row, c0, ly.aproj_b[n]);
           const float v1 = __uint_as_float(res.y) + red_val(red, 0, row, c0 + 1, ly.aproj_b[n + 1]);
@@ -520,13 +538,13 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
         VCAP_PHASE_IDS();
         const bool act = wg < nt_fc;
         if (compute && act) ln_rows<E>(a.base, a.o_h, M, ly.ln2_g, ly.ln2_b, a.ln_eps, dyn, wave, lane);
-        __syncthreads();
+        wg_barrier();
         if (compute && act) {
           f32x4 acc[2];
           mma_lds<E, NSL1, 2>(acc, wq, dyn, wave, lane);
           to_red<2>(red, acc, wave, lane);
         }
-        __syncthreads();
+        wg_barrier();
         if (compute && act) {
           const int j = tid >> 7, row = (tid >> 3) & 15, c0 = (tid & 7) * 2;
           const int t = wg + j * G;
@@ -564,7 +582,7 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
             acc[0] = mfma_frag(af[s], *reinterpret_cast<const u32x4*>(w5 + s * 1024), acc[0], (bf16_t*)nullptr);
           to_red<1>(red, acc, wave, lane);
         }
-        __syncthreads();
+        wg_barrier();
         if (compute && act && tid < 128 && row < M) {
           const float v0 = __uint_as_float(res.x) + red_val(red, 0, row, c0, ly.mproj_b[n]);
           const float v1 = __uint_as_float(res.y) + red_val(red, 0, row, c0 + 1, ly.mproj_b[n + 1]);
@@ -591,7 +609,7 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
         reinterpret_cast<unsigned*>(s_rep)[i] = 0u;
         reinterpret_cast<unsigned*>(s_ban)[i] = 0u;
       }
-      __syncthreads();
+      wg_barrier();
       if (compute) {
         for (int i = tid; i < M * a.hist_ld; i += kCompute) {
           const int m = i / a.hist_ld, tt = i - m * a.hist_ld;
@@ -604,7 +622,7 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
         }
         if (ntl > 0) ln_rows<E>(a.base, a.o_h, M, a.lnf_g, a.lnf_b, a.ln_eps, dyn, wave, lane);
       }
-      __syncthreads();
+      wg_barrier();
       float bv = -INFINITY;
       int bi = 0x7fffffff;
       const int row = tid >> 4, col = tid & 15;
@@ -616,7 +634,7 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
           mma_lds<E, NSL1, LMNTB>(acc, w, dyn, wave, lane);
           to_red<LMNTB>(red, acc, wave, lane);
         }
-        __syncthreads();
+        wg_barrier();
         if (compute && row < M) {
 #pragma unroll
           for (int j = 0; j < LMNTB; ++j) {
@@ -634,7 +652,7 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
             }
           }
         }
-        __syncthreads();
+        wg_barrier();
       };
       u32x4 wB[NQ];
       for (int gi = 0; gi < ngr; gi += 2) {
@@ -679,7 +697,7 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
           s_mv[wave] = bv;
           s_misc[4 + wave] = bi;
         }
-        __syncthreads();
+        wg_barrier();
         if (tid == 0) {
           for (int w = 1; w < kThreads / 64; ++w) argmax_take(bv, bi, s_mv[w], s_misc[4 + w]);
           int tok = bi;
@@ -692,7 +710,7 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
           s_misc[1] = tok;
           s_misc[2] = 0;
         }
-        __syncthreads();
+        wg_barrier();
         const int Lh = step + 1, ng = a.ngram;
         if (ng > 0 && Lh + 1 >= ng) {
           for (int i = tid; i + ng <= Lh; i += kThreads) {
@@ -701,7 +719,7 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
             if (match) st4(a.base, a.o_banned + (m * hl + atomicAdd(&s_misc[2], 1)) * 4, (unsigned)s_h[i + ng - 1]);
           }
         }
-        __syncthreads();
+        wg_barrier();
         if (tid == 0) st4(a.base, a.o_nbanned + m * 4, (unsigned)s_misc[2]);
         const int tok = s_misc[1];
         const int pos = min(a.S0 + step, a.n_pos - 1);
@@ -788,6 +806,13 @@ hipError_t vcap_decode_persist_dispatch(const PersistDesc& d, hipStream_t s) {
   if (E == 768) return launch_persist<768>(a, s);
   if (E == 1024) return launch_persist<1024>(a, s);
   return launch_persist<128>(a, s);
+}
+
+// diagnostic read-back of the stamps (not part of include/vcap.h): n values of [wg][phase][2]
+extern "C" int vcap_persist_stamps_read(unsigned long* dst, size_t n) {
+  const size_t cap = sizeof(g_persist_stamps) / sizeof(unsigned long);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_persist_stamps), (n < cap ? n : cap) * sizeof(unsigned long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 
 unsigned vcap_decode_persist_faults() {

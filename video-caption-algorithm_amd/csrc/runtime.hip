@@ -340,7 +340,13 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
       PersistDesc pd;
       memset(&pd, 0, sizeof(pd));
       pd.G = G; pd.M = B; pd.E = E; pd.H = d->n_head; pd.L = d->n_layer; pd.V = V; pd.S0 = S0; pd.maxp = maxp;
-      pd.n_pos = d->n_positions; pd.step0 = 1; pd.step1 = max_new; pd.ln_eps = d->ln_eps;
+      // (diagnostic: VCAP_PERSIST_STEPS=k runs steps 1 .. k-1 persistent and the rest as the chain)
+      static const int diag_steps = [] {
+        const char* e = std::getenv("VCAP_PERSIST_STEPS");
+        return e ? (int)std::strtol(e, nullptr, 10) : 0;
+      }();
+      const int step1 = diag_steps > 1 && diag_steps < max_new ? diag_steps : max_new;
+      pd.n_pos = d->n_positions; pd.step0 = 1; pd.step1 = step1; pd.ln_eps = d->ln_eps;
       pd.lnf_g = d->lnf_g; pd.lnf_b = d->lnf_b; pd.lm_head = d->lm_head; pd.wte = d->wte; pd.wpe = d->wpe;
       pd.h = w.h; pd.q = w.q; pd.attn = w.attn; pd.act = w.act; pd.kc = w.kc; pd.vc = w.vc;
       pd.page_elems = (long)page_elems;
@@ -351,7 +357,8 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
       pd.pval = w.pval; pd.pidx = w.pidx; pd.bar = w.persist;
       pd.layers = reinterpret_cast<const PersistLayer*>(d->layers);
       VCAP_TRY(vcap_decode_persist_dispatch(pd, s), "decode_persist");
-      break;
+      if (step1 == max_new) break;
+      step = step1;
     }
     const int S_new = step == 0 ? S0 : 1;
     const int past = step == 0 ? 0 : S0 + step - 1;

@@ -146,7 +146,7 @@ def cpu_baseline(sd, va, ga, frames_np, budget_s: float, max_new: int, beams: in
     return out
 
 
-PMC_FILES = ("r02_pmc.json", "r01_pmc.json")   # newest first
+PMC_FILES = ("r04_pmc.json", "r02_pmc.json", "r01_pmc.json")   # newest first
 
 
 def _pmc_file(M: int):
@@ -182,8 +182,9 @@ def pmc_summary(vit: str, gpt2: str, M: int, precision: str):
     name, d = _pmc_file(M)
     if d is None:
         return None
-    util = {k.split("<", 1)[1].rstrip(">"): round(v["mfma_util"], 3) for k, v in d["vit_kernels"].items()
-            if "gemm256" in k and v.get("mfma_util")}
+    # (r04 splits the attn-proj / fc2 launches of the shared <bf16, f32, 2> instantiation: "...2>[fc2]")
+    util = {k.split("<", 1)[1].replace(">", " ").strip(): round(v["mfma_util"], 3)
+            for k, v in d["vit_kernels"].items() if "gemm256" in k and v.get("mfma_util")}
     return {"source": f"profiles/{name} (rocprofv3 --pmc, separate passes, ViT launches of {M} rows)",
             "vit_gemm_mfma_util": util,
             "decode_hbm_bytes_per_token_step": d["decode"]["hbm_bytes_per_token_step"]}

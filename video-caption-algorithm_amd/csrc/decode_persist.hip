@@ -404,6 +404,11 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     wg_barrier();
     ++phase;
+    if ((a.flags & 32) && lane == 0) {   // diagnostic: agent release by every wave
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (a.flags & 32) wg_barrier();
     if (wave == 4) {
       if ((a.flags & 8) && lane == 0 && phase <= kStampPhases)
         g_persist_stamps[blockIdx.x][phase - 1][0] = __builtin_amdgcn_s_memrealtime();
@@ -437,6 +442,10 @@ __global__ __launch_bounds__(kThreads, 1) void vcap_decode_persist_kernel(Persis
       if (lane == 0) s_misc[0] = ok;
       if ((a.flags & 8) && lane == 0 && phase <= kStampPhases)
         g_persist_stamps[blockIdx.x][phase - 1][1] = __builtin_amdgcn_s_memrealtime();
+    }
+    if ((a.flags & 16) && lane == 0) {   // diagnostic: agent acquire (L1 invalidate) by every wave
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     wg_barrier();
     return s_misc[0] != 0;

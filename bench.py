@@ -478,6 +478,8 @@ def main():
                                                reserve_cus=0)
             for k in ("default_schedule", "strict_batch"):
                 pt[k].pop("latency_ms_stats")
+            print(f"sweep batch {bs}: default {pt['default_schedule']['value']:.1f}, strict "
+                  f"{pt['strict_batch']['value']:.1f} captions/s", file=sys.stderr, flush=True)
             sweep.append(pt)
             del vid
         torch.cuda.empty_cache()

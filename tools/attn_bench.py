@@ -32,5 +32,10 @@ for _ in range(7):
 ms = statistics.median(ts)
 fl = 4.0 * BT * H * NT * NT * 64
 print(f"attention BT={BT} N={NT} H={H}: {ms * 1e3:.1f} us  {fl / ms / 1e9:.1f} TF", flush=True)
+q, k, v = qkv.float().view(BT, NT, 3, H, 64).permute(2, 0, 3, 1, 4)
+ref = torch.nn.functional.scaled_dot_product_attention(q, k, v).permute(0, 2, 1, 3).reshape(BT * NT, H * 64)
+err = (out.float() - ref).abs()
+print(f"max |out - fp32 SDPA| {float(err.max()):.3e}  mean {float(err.mean()):.3e}  "
+      f"variant {os.environ.get('VCAP_ATTN_VARIANT', 'shipped')}", flush=True)
 if os.environ.get("DUMP"):
     torch.save(out.cpu(), os.environ["DUMP"])

@@ -319,13 +319,13 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
         const f32x4 d = xv[r][c] - mean;
-        ss += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+        ss += sumsq4(d);
       }
       const float rstd = rsqrtf(wave_sum(ss) / (float)K + a.ln_eps);
       const bool live = m0 + m < M;
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
-        const f32x4 y = live ? (xv[r][c] - mean) * rstd * gv[c] + bv[c] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        const f32x4 y = live ? ln_affine4(xv[r][c], mean, rstd, gv[c], bv[c]) : (f32x4){0.f, 0.f, 0.f, 0.f};
         const int byte = (c * 256 + lane * 4) * (int)sizeof(T);
         char* dst = dyn + (long)m * rowb + ((((byte >> 4) ^ (m & 15))) << 4) + (byte & 15);
         if constexpr (sizeof(T) == 2) {
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
         for (int ci = 0; ci < 4; ++ci)
           if (ci * 256 + lane * 4 < K) {
             const f32x4 d = xv[r][ci] - mean;
-            ss += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+            ss += sumsq4(d);
           }
         const float rstd = rsqrtf(wave_sum(ss) / (float)K + a.ln_eps);
         const bool live = m0 + ml < M;
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemm_lds_kernel(RowsGemmArgs a)
         for (int ci = 0; ci < 4; ++ci) {
           const int c = ci * 256 + lane * 4;
           if (c < K) {
-            const f32x4 y = live ? (xv[r][ci] - mean) * rstd * gv[ci] + bv[ci] : (f32x4){0.f, 0.f, 0.f, 0.f};
+            const f32x4 y = live ? ln_affine4(xv[r][ci], mean, rstd, gv[ci], bv[ci]) : (f32x4){0.f, 0.f, 0.f, 0.f};
             const int byte = c * (int)sizeof(T);
             char* dst = dyn + (long)ml * rowb + ((((byte >> 4) ^ (ml & 15))) << 4) + (byte & 15);
             if constexpr (sizeof(T) == 2) {
@@ -943,14 +943,14 @@ __global__ __launch_bounds__(256) void vcap_lm_head_stream_kernel(RowsGemmArgs a
     for (int c = 0; c < KC; ++c)
       if (c * 256 + lane * 4 < K) {
         const f32x4 d = xv[r][c] - mean;
-        ss += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+        ss += sumsq4(d);
       }
     const float rstd = rsqrtf(wave_sum(ss) / (float)K + a.ln_eps);
     const bool live = m < M;
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
       if (c * 256 + lane * 4 < K) {
-        const f32x4 y = live ? (xv[r][c] - mean) * rstd * gv[c] + bv[c] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        const f32x4 y = live ? ln_affine4(xv[r][c], mean, rstd, gv[c], bv[c]) : (f32x4){0.f, 0.f, 0.f, 0.f};
         const int byte = (c * 256 + lane * 4) * (int)sizeof(T);
         char* dst = dyn + (long)m * (K * (int)sizeof(T)) + ((((byte >> 4) ^ (m & 15))) << 4) + (byte & 15);
         if constexpr (sizeof(T) == 2) {
@@ -1186,7 +1186,7 @@ __global__ __launch_bounds__(256) void vcap_decode_attention_c64_kernel(const bf
   sc *= 0.125f;
   const bool live = lane < ctx;
   const float mx = wave_max(live ? sc : -INFINITY);
-  const float p = live ? __expf(sc - mx) : 0.f;
+  const float p = live ? __expf(sub_nc(sc, mx)) : 0.f;
   const float sum = wave_sum(p);
   s_p[wave][lane] = p;
   __builtin_amdgcn_wave_barrier();

@@ -141,14 +141,14 @@ VCAP_DEV void ln_rows(const char* base, int ox, int M, const float* g, const flo
     for (int c = 0; c < KC; ++c)
       if (c * 256 + lane * 4 < E) {
         const f32x4 d = xv[r][c] - mean;
-        ss += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+        ss += sumsq4(d);
       }
     const float rstd = rsqrtf(wave_sum(ss) / (float)E + eps);
     const bool live = m < M;
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
       if (c * 256 + lane * 4 < E) {
-        const f32x4 y = live ? (xv[r][c] - mean) * rstd * gv[c] + bv[c] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        const f32x4 y = live ? ln_affine4(xv[r][c], mean, rstd, gv[c], bv[c]) : (f32x4){0.f, 0.f, 0.f, 0.f};
         const int byte = (c * 256 + lane * 4) * 2;
         char* dst = dyn + (long)m * (E * 2) + ((((byte >> 4) ^ (m & 15))) << 4) + (byte & 15);
         *reinterpret_cast<u32x2*>(dst) = (u32x2){pack_bf2(y.x, y.y), pack_bf2(y.z, y.w)};
@@ -253,7 +253,7 @@ VCAP_DEV void attn_item(const PersistArgs& a, int okc, int ovc, int m, int h, in
     sc *= 0.125f;
     const bool live = lane < ctx;
     const float mx = wave_max(live ? sc : -INFINITY);
-    const float p = live ? __expf(sc - mx) : 0.f;
+    const float p = live ? __expf(sub_nc(sc, mx)) : 0.f;
     sum = wave_sum(p);
     s_p[lane] = p;
     __builtin_amdgcn_wave_barrier();

@@ -25,6 +25,8 @@
 //    follow it in both groups;
 //  * the MFMA takes the weight fragment as its A operand, so each lane ends up holding 4
 //    consecutive output COLUMNS of one row: vectorised bias / residual / store epilogue.
+#include <cstdlib>
+
 #include "vcap_common.h"
 #include "vcap_kernels.h"
 
@@ -293,7 +295,20 @@ __global__ __launch_bounds__(512) void vcap_gemm256_kernel(const TIn* __restrict
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
-  const int m0 = (wgid / tiles_n) * TM, n0 = (wgid % tiles_n) * TN;
+  // tile order: row-major (consecutive ids share an A row panel), or column groups of w tile columns
+  // (an XCD's run of ids then re-reads only w weight tiles: its L2 keeps them across rounds instead
+  // of re-fetching all tiles_n of them every round; A panels are read once per group)
+  int mt, nt;
+  if (epi.colgroup > 0) {
+    const int w = epi.colgroup, per = w * tiles_m;
+    const int g = wgid / per, rem = wgid - g * per;
+    mt = rem / w;
+    nt = g * w + (rem - (rem / w) * w);
+  } else {
+    mt = wgid / tiles_n;
+    nt = wgid - mt * tiles_n;
+  }
+  const int m0 = mt * TM, n0 = nt * TN;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS-DMA bases stay scalar
@@ -515,9 +530,21 @@ static hipError_t launch256_epi(const void* A, long lda, const void* W, long ldw
     if (e != hipSuccess) return e;
     configured = true;
   }
-  const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  const int tiles_n = (N + TN - 1) / TN;
+  const int tiles = ((M + TM - 1) / TM) * tiles_n;
+  GemmEpi e = epi;
+  e.colgroup = 0;
+  {
+    // column-group tile order (VCAP_GEMM_COLGROUP=w, for the GELU GEMM - fc1 - whose 12 weight
+    // tiles (4.7 MB) do not fit one XCD's 4 MB L2 beside its A panels)
+    static const int w = [] {
+      const char* v = std::getenv("VCAP_GEMM_COLGROUP");
+      return v ? (int)std::strtol(v, nullptr, 10) : 0;
+    }();
+    if (EPI == 1 && w > 0 && w < tiles_n && tiles_n % w == 0) e.colgroup = w;
+  }
   hipLaunchKernelGGL((vcap_gemm256_kernel<TIn, TOut, EPI>), dim3(tiles), dim3(512), lds, s, (const TIn*)A, lda,
-                     (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, epi);
+                     (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, e);
   return hipGetLastError();
 }
 

@@ -21,6 +21,9 @@ struct GemmEpi {
   // [split][M][N]; the partials are summed in split order by a second kernel.  nullptr: no split.
   float* splitk_ws;
   size_t splitk_bytes;
+  // 256x256 kernel tile order (set by its dispatcher): 0 = row-major over (row panel, column tile);
+  // w > 0 = column groups of w tile columns, row-major inside a group
+  int colgroup;
 };
 
 enum { PRO_LN = 0, PRO_DIRECT = 1 };

@@ -146,7 +146,7 @@ def cpu_baseline(sd, va, ga, frames_np, budget_s: float, max_new: int, beams: in
     return out
 
 
-PMC_FILES = ("r04_pmc.json", "r02_pmc.json", "r01_pmc.json")   # newest first
+PMC_FILES = ("r04_pmc_colgroup.json", "r04_pmc.json", "r02_pmc.json", "r01_pmc.json")   # newest first
 
 
 def _pmc_file(M: int):

@@ -534,14 +534,27 @@ static hipError_t launch256_epi(const void* A, long lda, const void* W, long ldw
   const int tiles = ((M + TM - 1) / TM) * tiles_n;
   GemmEpi e = epi;
   e.colgroup = 0;
-  {
-    // column-group tile order (VCAP_GEMM_COLGROUP=w, for the GELU GEMM - fc1 - whose 12 weight
-    // tiles (4.7 MB) do not fit one XCD's 4 MB L2 beside its A panels)
-    static const int w = [] {
+  if (EPI == 1) {
+    // column-group tile order for the GELU GEMM (fc1), whose weight tiles do not fit one XCD's 4 MB
+    // L2 beside its A panels (ViT-B: 12 x 384 KB): the widest group of whole tile columns dividing
+    // tiles_n with <= 2.5 MB of weights, so an XCD keeps its group's tiles across rounds.  Measured
+    // (profiles/r04_gemm_colgroup_ab.txt, 16-video fc1): FETCH 426 -> 294 MB per launch, 310 -> 306 us
+    // in the pipelined bench, equal alone.  VCAP_GEMM_COLGROUP=w overrides (0: row-major).
+    static const int env_w = [] {
       const char* v = std::getenv("VCAP_GEMM_COLGROUP");
-      return v ? (int)std::strtol(v, nullptr, 10) : 0;
+      return v ? (int)std::strtol(v, nullptr, 10) : -1;
     }();
-    if (EPI == 1 && w > 0 && w < tiles_n && tiles_n % w == 0) e.colgroup = w;
+    int w = env_w;
+    if (w < 0) {
+      const long tile_bytes = (long)TN * K * (long)sizeof(TIn);
+      w = 0;
+      for (int c = tiles_n - 1; c >= 1; --c)
+        if (tiles_n % c == 0 && c * tile_bytes <= 2560L * 1024) {
+          w = c;
+          break;
+        }
+    }
+    if (w > 0 && w < tiles_n && tiles_n % w == 0) e.colgroup = w;
   }
   hipLaunchKernelGGL((vcap_gemm256_kernel<TIn, TOut, EPI>), dim3(tiles), dim3(512), lds, s, (const TIn*)A, lda,
                      (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, e);

@@ -1186,7 +1186,7 @@ __global__ __launch_bounds__(256) void vcap_decode_attention_c64_kernel(const bf
   sc *= 0.125f;
   const bool live = lane < ctx;
   const float mx = wave_max(live ? sc : -INFINITY);
-  const float p = live ? __expf(sub_nc(sc, mx)) : 0.f;
+  const float p = live ? __expf(sc - mx) : 0.f;
   const float sum = wave_sum(p);
   s_p[wave][lane] = p;
   __builtin_amdgcn_wave_barrier();

@@ -253,7 +253,7 @@ VCAP_DEV void attn_item(const PersistArgs& a, int okc, int ovc, int m, int h, in
     sc *= 0.125f;
     const bool live = lane < ctx;
     const float mx = wave_max(live ? sc : -INFINITY);
-    const float p = live ? __expf(sub_nc(sc, mx)) : 0.f;
+    const float p = live ? __expf(sc - mx) : 0.f;
     sum = wave_sum(p);
     s_p[lane] = p;
     __builtin_amdgcn_wave_barrier();

@@ -4,9 +4,9 @@ workgroups with grid barriers between phases; opt-in, measured slower than the l
 bit-identical, at the bench shapes (B = 8 and 16 rows of GPT-2 small), raw greedy, GPT-2-medium and
 the tiny config, for several grid sizes.  The launch chain itself is pinned to the reference
 (test_gpu_bf16.py teacher-forced bf16, test_gpu_parity.py fp32 token-exact).  (Bit equality holds
-because every decode kernel computes its LayerNorm and attention exp argument through the same
-contraction-free helpers, vcap_common.h sumsq4 / ln_affine4 / sub_nc: left to the compiler's FMA
-contraction, single rows differed by up to 1.3e-2 from some step on - profiles/r04_persistent_decode.txt.)"""
+because every decode kernel computes its LayerNorm through the same explicit-fma helpers,
+vcap_common.h sumsq4 / ln_affine4: left to the compiler's FMA contraction, single rows differed by up
+to 1.3e-2 from some step on - profiles/r04_persistent_decode.txt.)"""
 import dataclasses
 
 import numpy as np

@@ -208,7 +208,8 @@ struct PersistArgs {
   float* logits_out;
   unsigned* bar;
   const PersistLayer* layers;  // device copy (vcap_persist_layers_kernel)
-  int flags;                   // diagnostics (VCAP_PERSIST_FLAGS): 1 barriers only, 4 no s_sleep in polls
+  int flags;                   // diagnostics (VCAP_PERSIST_FLAGS): 1 barriers only, 4 no s_sleep in polls,
+                               // 8 stamps, 16 / 32 agent acquire / release fences at every barrier
 };
 
 struct PersistLayers {

@@ -462,8 +462,7 @@ template <int KT, int KE, int WAVES, bool MXO, bool PIPE = false>
 __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(const bf16_t* __restrict__ qkv,
                                                                              void* __restrict__ out, int N, int H,
                                                                              uint8_t* __restrict__ oscale,
-                                                                             int groups, int cls_only, int split_lo,
-                                                                             int split_n) {
+                                                                             int groups, int cls_only) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NP = KT * 16;
   constexpr int NS = KE * 16;  // staged key rows (the all-padding last tile is never read)
@@ -472,21 +471,7 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
   char* Ks = smem;
   char* Vs = smem + NS * 128;
 
-  // (frame, head) pair and its query-tile range.  split_n > 0 (VCAP_ATTN_DESYNC): pairs
-  // [split_lo, split_lo + split_n) - the second workgroup of every CU in the first round - run
-  // only their first qh query tiles, and split_n workgroups appended to the grid run the rest, so
-  // the two workgroups sharing a CU stay half a lifetime apart: one's K/V load overlaps the
-  // other's compute instead of every CU loading at once.
-  const int qtiles = cls_only ? 1 : (N + 15) / 16;
-  const int qh = (qtiles + 1) / 2;
-  const int n_pairs = gridDim.x - split_n;
-  int bh = blockIdx.x, qt0 = 0, qt1 = qtiles;
-  if (bh >= n_pairs) {
-    bh = split_lo + (bh - n_pairs);
-    qt0 = qh;
-  } else if (bh >= split_lo && bh < split_lo + split_n) {
-    qt1 = qh;
-  }
+  const int bh = blockIdx.x;
   const int bt = bh / H, h = bh - bt * H;
   const int D = H * 64;
   const long ld = 3L * D;
@@ -505,10 +490,11 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
   }
   (void)NP;
   // ---- this wave's Q fragments
+  const int qtiles = cls_only ? 1 : (N + 15) / 16;
   u32x4 qf[QT_MAX][2];
 #pragma unroll
   for (int i = 0; i < QT_MAX; ++i) {
-    const int q = min((qt0 + wave + i * WAVES) * 16 + fr, N - 1);
+    const int q = min((wave + i * WAVES) * 16 + fr, N - 1);
 #pragma unroll
     for (int s = 0; s < 2; ++s) qf[i][s] = *reinterpret_cast<const u32x4*>(base + (long)q * ld + s * 32 + fg * 8);
   }
@@ -517,8 +503,8 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
 
 #pragma unroll
   for (int i = 0; i < QT_MAX; ++i) {
-    const int qt = qt0 + wave + i * WAVES;
-    if (qt >= qt1) break;
+    const int qt = wave + i * WAVES;
+    if (qt >= qtiles) break;
     f32x4 o[4];
     float inv;
     if constexpr (PIPE) {
@@ -545,22 +531,8 @@ static hipError_t launch_attn_bf16(const void* qkv, void* out, int BT, int N, in
     configured = true;
   }
   const int groups = ((cls_only ? BT : BT * N) + 255) / 256;  // scale rows = output rows
-  static const int desync = [] {
-    const char* e = std::getenv("VCAP_ATTN_DESYNC");
-    return e ? (int)std::strtol(e, nullptr, 10) : 0;
-  }();
-  const int pairs = BT * H;
-  int split_lo = 0, split_n = 0;
-  if (desync && !cls_only && (N + 15) / 16 >= 2) {
-    const int cus = vcap_stream_cus(s);
-    if (pairs >= 2 * cus) {
-      split_lo = cus;
-      split_n = cus;
-    }
-  }
-  hipLaunchKernelGGL((vcap_vit_attention_bf16_kernel<KT, KE, WAVES, MXO, PIPE>), dim3(pairs + split_n),
-                     dim3(WAVES * 64), lds, s, (const bf16_t*)qkv, out, N, H, oscale, groups, cls_only, split_lo,
-                     split_n);
+  hipLaunchKernelGGL((vcap_vit_attention_bf16_kernel<KT, KE, WAVES, MXO, PIPE>), dim3(BT * H), dim3(WAVES * 64), lds, s,
+                     (const bf16_t*)qkv, out, N, H, oscale, groups, cls_only);
   return hipGetLastError();
 }
 

@@ -180,3 +180,24 @@ def test_driver_entry_scripts_compile_cleanly():
         with warnings.catch_warnings():
             warnings.simplefilter("error")
             compile((root / name).read_text(), name, "exec")
+
+
+def test_bench_reads_the_newest_pmc_pass():
+    """bench.py's `roofline.traffic` and `pmc` fields come from the newest committed PMC pass taken
+    on the configs[1] encode shape (50432-row launches): this round's, with the fc1 tile order and
+    the attn-proj / fc2 split of the shared <bf16, f32, 2> grid."""
+    import importlib.util
+    root = Path(__file__).resolve().parents[1]
+    spec = importlib.util.spec_from_file_location("bench_mod", root / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    name, d = bench._pmc_file(50432)
+    assert name == bench.PMC_FILES[0] and d["vit_rows"] == 50432
+    t = bench.fc1_traffic(50432, 3072, 768)
+    algorithmic = 2 * (50432 * 768 + 3072 * 768) + 2 * 50432 * 3072   # A + W read, bf16 C written
+    assert t is not None and algorithmic < t < 1.6 * algorithmic
+    s = bench.pmc_summary("vit_base_patch16_224", "gpt2", 50432, "bf16")
+    assert s["source"].startswith(f"profiles/{name}")
+    assert {"unsigned short, float, 2 [attn-proj]", "unsigned short, float, 2 [fc2]"} <= set(s["vit_gemm_mfma_util"])
+    # another launch shape reads the pass taken on that shape (r01: 25216-row launches), labelled so
+    assert "r04" not in bench.pmc_summary("vit_base_patch16_224", "gpt2", 25216, "bf16")["source"]

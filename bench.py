@@ -146,6 +146,7 @@ def cpu_baseline(sd, va, ga, frames_np, budget_s: float, max_new: int, beams: in
     return out
 
 
+STRICT_RESERVE = 32   # CUs the strict_batch leg reserves off its encode stream
 PMC_FILES = ("r04_pmc_colgroup.json", "r04_pmc.json", "r02_pmc.json", "r01_pmc.json")   # newest first
 
 
@@ -459,10 +460,12 @@ def main():
     # decode per batch (no two-batch coalescing), two decode lanes, timed like `value`
     strict = None
     if args.strict_steps > 0 and not args.serial:
+        # 32 CUs reserved off the encode stream, as for the coalesced schedule: 1066 vs 928 captions/s
+        # and p50 22.1 vs 24.6 ms unreserved (profiles/r04_strict_reserve_sweep.txt)
         strict = time_schedule(enc, pre, dec, cfg, video, prompt, dev, world, args.strict_steps, args.warmup,
-                               dec_lanes=args.dec_lanes, dec_group=1, enc_group=1, reserve_cus=0)
+                               dec_lanes=args.dec_lanes, dec_group=1, enc_group=1, reserve_cus=STRICT_RESERVE)
         strict["schedule"] = (f"one {B}-video encode + one {B}-row decode graph per batch, {args.dec_lanes} decode "
-                              f"lanes, no coalescing")
+                              f"lanes, encode stream off {STRICT_RESERVE} CUs, no coalescing")
     sweep = None
     if args.batch_sizes:
         sweep = []
@@ -475,7 +478,7 @@ def main():
                                                    enc_group=eg, reserve_cus=32 if eg == 2 else 0)
             pt["strict_batch"] = time_schedule(enc, pre, dec, cfg, vid, prompt, dev, world, args.sweep_steps,
                                                args.warmup, dec_lanes=args.dec_lanes, dec_group=1, enc_group=1,
-                                               reserve_cus=0)
+                                               reserve_cus=STRICT_RESERVE)
             for k in ("default_schedule", "strict_batch"):
                 pt[k].pop("latency_ms_stats")
             print(f"sweep batch {bs}: default {pt['default_schedule']['value']:.1f}, strict "

@@ -38,6 +38,63 @@ from . import _native as N
 from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, _Workspace
 
 
+# One set of streams per (device, reservation, confinement, lanes) for the whole process, reused by
+# every pipeline with that schedule.  Measured: pipelines that each created fresh streams after
+# earlier ones had been closed sometimes ran serialised - an 8-video schedule following another in
+# one bench process read 291 instead of ~1090 captions/s (profiles/r04_stream_reuse.txt) - most
+# likely their encode stream and a decode lane sharing one of the process's 4 hardware queues
+# (streams are spread over them in creation order).  Reusing the first set keeps the queue layout
+# every measurement was taken with.
+_STREAM_SETS: dict = {}
+
+
+def _stream_set(device, reserve_cus: int, confine_decode: bool, lanes: int):
+    key = (torch.device(device).index or 0, reserve_cus, confine_decode and reserve_cus > 0, lanes)
+    if key in _STREAM_SETS:
+        return _STREAM_SETS[key][:2]
+    lo, hi = torch.cuda.Stream.priority_range()
+    handles = []
+    with torch.cuda.device(device):
+        if reserve_cus > 0:
+            # the encode kept off `reserve_cus` CUs (a CU-masked stream) so the decode always finds some
+            h = C.c_void_p()
+            N.check(N.lib().vcap_stream_create_cu_reserved(int(reserve_cus), C.byref(h)), "masked stream")
+            handles.append(h.value)
+            s_enc = torch.cuda.ExternalStream(h.value, device=device)
+        else:
+            s_enc = torch.cuda.Stream(device, priority=lo)
+        if confine_decode and reserve_cus > 0:
+            # decode streams masked to exactly the reserved CUs: decode workgroups never take an
+            # encode CU between two GEMM workgroups
+            words = (torch.cuda.get_device_properties(device).multi_processor_count + 31) // 32
+            mask = (C.c_uint32 * words)()
+            for c in range(reserve_cus):
+                mask[c // 32] |= 1 << (c % 32)
+            s_decs = []
+            for _ in range(lanes):
+                h = C.c_void_p()
+                N.check(N.lib().vcap_stream_create_cu_mask(mask, words, C.byref(h)), "decode stream")
+                handles.append(h.value)
+                s_decs.append(torch.cuda.ExternalStream(h.value, device=device))
+        else:
+            # the decode chain is latency-bound: its lanes get the higher priority (normal priority
+            # measured the same, 1224-1228 captions/s either way, r03)
+            s_decs = [torch.cuda.Stream(device, priority=hi) for _ in range(lanes)]
+    _STREAM_SETS[key] = (s_enc, s_decs, handles)
+    return s_enc, s_decs
+
+
+def release_streams() -> None:
+    """Destroy the CU-masked streams of every cached stream set (after all pipelines are closed)."""
+    for s_enc, s_decs, handles in _STREAM_SETS.values():
+        s_enc.synchronize()
+        for s in s_decs:
+            s.synchronize()
+        for h in handles:
+            N.check(N.lib().vcap_stream_destroy(h), "stream destroy")
+    _STREAM_SETS.clear()
+
+
 class CaptionPipeline:
     def __init__(self, encoder: HipViTEncoder, prefix: HipPrefix, decoder: HipGPT2Decoder, cfg: GenConfig,
                  batch: int, prompt_ids: Sequence[int], device, depth: int = 2, gather=None,
@@ -62,32 +119,7 @@ class CaptionPipeline:
         # The decode chain is latency-bound: give its stream the higher priority so its small
         # workgroups are dispatched as soon as encode GEMM workgroups retire, and optionally keep
         # the encode off `reserve_cus` CUs (a CU-masked stream) so the decode always finds some.
-        lo, hi = torch.cuda.Stream.priority_range()
-        self._masked = None
-        with torch.cuda.device(self.device):
-            if reserve_cus > 0:
-                h = C.c_void_p()
-                N.check(N.lib().vcap_stream_create_cu_reserved(int(reserve_cus), C.byref(h)), "masked stream")
-                self._masked = h.value
-                self.s_enc = torch.cuda.ExternalStream(self._masked, device=self.device)
-            else:
-                self.s_enc = torch.cuda.Stream(self.device, priority=lo)
-            self._dec_handles = []
-            if confine_decode and reserve_cus > 0:
-                # decode streams masked to exactly the reserved CUs: decode workgroups never take
-                # an encode CU between two GEMM workgroups
-                words = (torch.cuda.get_device_properties(self.device).multi_processor_count + 31) // 32
-                mask = (C.c_uint32 * words)()
-                for c in range(reserve_cus):
-                    mask[c // 32] |= 1 << (c % 32)
-                for _ in range(self.lanes):
-                    h = C.c_void_p()
-                    N.check(N.lib().vcap_stream_create_cu_mask(mask, words, C.byref(h)), "decode stream")
-                    self._dec_handles.append(h.value)
-                self.s_decs = [torch.cuda.ExternalStream(h, device=self.device) for h in self._dec_handles]
-            else:
-                # (normal-priority decode lanes measured the same: 1224-1228 captions/s either way, r03)
-                self.s_decs = [torch.cuda.Stream(self.device, priority=hi) for _ in range(self.lanes)]
+        self.s_enc, self.s_decs = _stream_set(self.device, int(reserve_cus), bool(confine_decode), self.lanes)
         self.s_dec = self.s_decs[0]
         # the encoder / decoder workspaces are shared with serial calls made on the creating stream:
         # nothing of the pipeline may start before that stream's pending work has finished
@@ -202,11 +234,6 @@ class CaptionPipeline:
             s.synchronize()
 
     def close(self) -> None:
-        """Drain both streams and release the CU-masked encode stream (if one was created)."""
+        """Drain the streams.  The streams themselves stay in the per-process set (_stream_set) for the
+        next pipeline with the same schedule; release_streams() destroys them."""
         self.synchronize()
-        if self._masked is not None:
-            N.check(N.lib().vcap_stream_destroy(self._masked), "stream destroy")
-            self._masked = None
-        for h in self._dec_handles:
-            N.check(N.lib().vcap_stream_destroy(h), "stream destroy")
-        self._dec_handles = []

@@ -556,14 +556,6 @@ static hipError_t launch256_epi(const void* A, long lda, const void* W, long ldw
     }
     if (w > 0 && w < tiles_n && tiles_n % w == 0) e.colgroup = w;
   }
-  if (EPI == 0) {
-    // (diagnostic: VCAP_GEMM_COLGROUP_QKV=w groups the plain bf16-out GEMM - QKV - the same way)
-    static const int qkv_w = [] {
-      const char* v = std::getenv("VCAP_GEMM_COLGROUP_QKV");
-      return v ? (int)std::strtol(v, nullptr, 10) : 0;
-    }();
-    if (qkv_w > 0 && qkv_w < tiles_n && tiles_n % qkv_w == 0) e.colgroup = qkv_w;
-  }
   hipLaunchKernelGGL((vcap_gemm256_kernel<TIn, TOut, EPI>), dim3(tiles), dim3(512), lds, s, (const TIn*)A, lda,
                      (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, e);
   return hipGetLastError();

@@ -96,8 +96,6 @@ def parse():
                     help="comma list (the reference's --batch-sizes sweep, core/scripts/benchmark_baseline.py:"
                          "486-493): time the default schedule and the strict per-batch schedule at each batch size")
     ap.add_argument("--sweep-steps", type=int, default=24, help="batches timed per --batch-sizes point")
-    ap.add_argument("--uc-decode-weights", action="store_true",
-                    help="experimental: decoder GEMV weights in uncached device memory")
     ap.add_argument("--dump-ids", default="",
                     help="rank 0 saves every timed batch's ids (gathered over ranks: [world*steps, B, max_new]) "
                          "to this .npy path")
@@ -362,8 +360,6 @@ def main():
     enc = HipViTEncoder(sd, va, args.precision, dev, mx_gemms=mx_gemms)
     pre = HipPrefix(sd, ga.n_embd, device=dev)
     dec = HipGPT2Decoder(sd, ga, "bf16" if args.precision == "fp8" else args.precision, dev)
-    if args.uc_decode_weights:
-        dec.relocate_weights_uncached()
     if args.decode == "hf_greedy":
         cfg = GenConfig(args.max_new, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, not args.no_graph,
                         num_beams=args.beams)

@@ -282,36 +282,6 @@ class HipGPT2Decoder:
         self._stable = {}             # (B, max_new) -> persistent prefix / ids buffers (graph reuse)
         torch.cuda.synchronize(dev)   # packing ran on the current stream; decodes may use others
 
-    def relocate_weights_uncached(self) -> None:
-        """Experimental (bench.py --uc-decode-weights): move the rows-packed GEMV weights and the
-        tied lm_head into uncached device memory (hipExtMallocWithFlags(hipDeviceMallocUncached)),
-        so the decode's once-per-step weight stream bypasses L2 and the Infinity Cache the encode
-        GEMMs re-read their operands from."""
-        import ctypes as CT
-        hip = CT.CDLL("libamdhip64.so")
-        hip.hipExtMallocWithFlags.argtypes = [CT.POINTER(CT.c_void_p), CT.c_size_t, CT.c_uint]
-        hip.hipMemcpy.argtypes = [CT.c_void_p, CT.c_void_p, CT.c_size_t, CT.c_int]
-        torch.cuda.synchronize(self.device)
-        self._uc = getattr(self, "_uc", [])
-
-        def move(ptr: int) -> int:
-            t = next(t for t in self._keep if t.data_ptr() == ptr)
-            n = t.numel() * t.element_size()
-            out = CT.c_void_p()
-            if hip.hipExtMallocWithFlags(CT.byref(out), n, 0x3) != 0:
-                raise RuntimeError("hipExtMallocWithFlags(uncached) failed")
-            if hip.hipMemcpy(out, CT.c_void_p(ptr), n, 3) != 0:   # hipMemcpyDeviceToDevice
-                raise RuntimeError("hipMemcpy failed")
-            self._uc.append(out.value)
-            return out.value
-
-        for i in range(self.arch.n_layer):
-            ly = self.layers[i]
-            ly.attn_w, ly.aproj_w = move(ly.attn_w), move(ly.aproj_w)
-            ly.fc_w, ly.mproj_w = move(ly.fc_w), move(ly.mproj_w)
-        self.desc.lm_head = move(self.lm_head.data_ptr())
-        torch.cuda.synchronize(self.device)
-
     def _pack(self, w: torch.Tensor) -> torch.Tensor:
         """[N, K] device weight -> rows-packed copy (MFMA-fragment order, csrc/decode.hip)."""
         rows, k = w.shape

@@ -180,6 +180,33 @@ def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group, egroup):
         pipe.close()
 
 
+def test_pipelines_reuse_one_stream_set_per_schedule(device):
+    """Pipelines with the same schedule reuse one set of streams for the process (vcap/pipeline.py
+    _stream_set: fresh streams per pipeline measured serialised, profiles/r04_stream_reuse.txt);
+    a second pipeline after the first is closed still gives the serial ids."""
+    from vcap.pipeline import CaptionPipeline
+    meta, g, va, ga, sd, frames, enc, pre, dec = _models("bf16", device)
+    video = torch.from_numpy(frames).to(device)
+    _, pre_serial = enc.encode(video, pre)
+    ids_serial = dec.generate_ids(pre_serial, [ga.bos_token_id], _hf_cfg(ga)).clone()
+    cfg = _hf_cfg(ga, max_blocks=96)
+    mk = lambda r: CaptionPipeline(enc, pre, dec, cfg, video.shape[0], [ga.bos_token_id], device,  # noqa: E731
+                                   reserve_cus=r, dec_lanes=2, dec_group=1, enc_group=1)
+    a = mk(32)
+    streams = (a.s_enc, list(a.s_decs))
+    a.close()
+    b, c = mk(32), mk(0)
+    try:
+        assert b.s_enc is streams[0] and b.s_decs == streams[1]
+        assert c.s_enc is not b.s_enc
+        slots = [b.submit(video) for _ in range(3)]
+        b.synchronize()
+        assert all(torch.equal(b.result(s), ids_serial) for s in slots)
+    finally:
+        b.close()
+        c.close()
+
+
 # ------------------------------------------------------------------ per-kernel tests at bench shapes
 
 def _rand(shape, seed, scale=1.0, device="cuda"):

@@ -192,13 +192,7 @@ VCAP_DEV void epilogue256(const f32x4 (&acc)[2][2][4][2], int m0, int n0, int wr
           const uint32_t r0 = (uint32_t)xor16_i((int)(odd ? p[0][0] : p[1][0]));
           const uint32_t r1 = (uint32_t)xor16_i((int)(odd ? p[0][1] : p[1][1]));
           const u32x4 o = odd ? (u32x4){r0, r1, p[1][0], p[1][1]} : (u32x4){p[0][0], p[0][1], r0, r1};
-          if (m < M && nb < N) {
-            u32x4* dst = reinterpret_cast<u32x4*>(C + (long)m * ldc + col);
-            if (epi.store_wt)
-              asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(dst), "v"(o) : "memory");
-            else
-              out_store(dst, o);
-          }
+          if (m < M && nb < N) out_store(reinterpret_cast<u32x4*>(C + (long)m * ldc + col), o);
         }
       }
   } else if constexpr (EPI == 2) {
@@ -540,7 +534,6 @@ static hipError_t launch256_epi(const void* A, long lda, const void* W, long ldw
   const int tiles = ((M + TM - 1) / TM) * tiles_n;
   GemmEpi e = epi;
   e.colgroup = 0;
-  e.store_wt = 0;
   if (EPI == 1) {
     // column-group tile order for the GELU GEMM (fc1), whose weight tiles do not fit one XCD's 4 MB
     // L2 beside its A panels (ViT-B: 12 x 384 KB): the widest group of whole tile columns dividing
@@ -562,11 +555,6 @@ static hipError_t launch256_epi(const void* A, long lda, const void* W, long ldw
         }
     }
     if (w > 0 && w < tiles_n && tiles_n % w == 0) e.colgroup = w;
-    static const int wt = [] {
-      const char* v = std::getenv("VCAP_GEMM_STORE_WT");
-      return v ? (int)std::strtol(v, nullptr, 10) : 0;
-    }();
-    e.store_wt = wt;
   }
   hipLaunchKernelGGL((vcap_gemm256_kernel<TIn, TOut, EPI>), dim3(tiles), dim3(512), lds, s, (const TIn*)A, lda,
                      (const TIn*)W, ldw, (TOut*)C, ldc, M, N, K, e);

@@ -24,7 +24,6 @@ struct GemmEpi {
   // 256x256 kernel tile order (set by its dispatcher): 0 = row-major over (row panel, column tile);
   // w > 0 = column groups of w tile columns, row-major inside a group
   int colgroup;
-  int store_wt;   // diagnostic: bf16 outputs stored write-through (sc1 nt) instead of nt alone
 };
 
 enum { PRO_LN = 0, PRO_DIRECT = 1 };

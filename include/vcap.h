@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 10
+#define VCAP_ABI_VERSION 11
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -119,11 +119,11 @@ typedef struct vcap_gen_params {
   int max_blocks;            /* 0: whole-chip grids; > 0: cap the projection GEMV grids near this
                                 many workgroups (wider tiles per workgroup) - for a decode that
                                 shares the GPU with an encode holding most CUs */
-  int persistent;            /* greedy bf16 decodes of <= 16 rows: 0 = one launch per decode kernel
-                                (~62 per token step); > 0 = steps 1.. as ONE persistent launch of
-                                this many workgroups, one per CU (csrc/decode_persist.hip, ids and
-                                logits bit-identical); < 0 = auto (VCAP_PERSIST_G or 128).  Other
-                                decodes ignore it. */
+  int split_attention;       /* 0: bf16 decode steps of <= 16 rows run each layer's causal attention
+                                inside its c_attn launch (the last workgroup to store a head's
+                                q / k / v columns attends that head: one launch per layer fewer);
+                                1: c_attn and attention as two launches (same arithmetic, ids and
+                                logits bit-identical; A/B runs and tests) */
 } vcap_gen_params;
 
 const char* vcap_last_error(void);
@@ -239,9 +239,6 @@ int vcap_gpt2_sample(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const v
                      float* logits_out, float* warped_out, const int* force_ids, void* workspace, size_t ws_bytes,
                      void* stream);
 void vcap_graph_cache_clear(void);
-/* persistent-decode grid barriers that gave up (bounded spin, 0.5 s) since the library loaded: a
- * nonzero value means some decode returned early and its ids are not valid (sticky counter). */
-unsigned vcap_decode_faults(void);
 /* number of instantiated decode graphs held by the cache (bounded LRU, VCAP_GRAPH_CACHE_MAX) */
 int vcap_graph_cache_size(void);
 /* decoder rows one call may carry: B * (prefix + prompt) at the prefill, B * num_beams per step */

@@ -69,28 +69,36 @@ def test_caption_sharded_rccl_one_rank(tmp_path):
     assert res["world"] == 1 and np.array_equal(got[:, :exp.shape[1]], exp)
 
 
-def test_bench_two_ranks_gloo(tmp_path, device):
-    """The N>1 bench path (torchrun, one process per rank, sharded videos, decode-lane id copies,
-    ONE end-of-run all-gather, MAX-over-ranks timing) rehearsed with 2 ranks sharing the box's
-    GPU over gloo (VCAP_BENCH_DIST_BACKEND): rank 0 prints one JSON line for n_gpus = 2, and the
-    ids it gathered are, for every timed batch of every rank, the ids a single-process serial
-    bf16 run computes on that rank's frames (bench.py seeds rank r's videos with 1000 + r)."""
+@pytest.mark.parametrize("launcher", ["self", "torchrun"])
+def test_bench_two_ranks_gloo(tmp_path, device, launcher):
+    """The N>1 bench path (one process per rank, sharded videos, decode-lane id copies, ONE
+    end-of-run all-gather, MAX-over-ranks timing) rehearsed with 2 ranks sharing the box's GPU
+    over gloo (VCAP_BENCH_DIST_BACKEND), started either by `python bench.py --gpus 2` itself (no
+    torchrun: the driver's command shape) or by torchrun: rank 0 prints one JSON line for
+    n_gpus = 2, and the ids it gathered are, for every timed batch of every rank, the ids a
+    single-process serial bf16 run computes on that rank's frames (bench.py seeds rank r's
+    videos with 1000 + r)."""
     import torch
     from vcap import configs, prng, weights
     from vcap.model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder
     steps = 4
     dump = tmp_path / "ids.npy"
-    env = dict(os.environ, VCAP_BENCH_DIST_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(HERE.parent / "bench.py"), "--gpus", "2",
-           "--steps", str(steps), "--warmup", "2", "--cpu-baseline-s", "0", "--no-parity", "--no-decode-alone",
-           "--host-e2e", "0", "--strict-steps", "2", "--dump-ids", str(dump)]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    env["VCAP_BENCH_DIST_BACKEND"] = "gloo"
+    run = ([sys.executable] if launcher == "self" else
+           [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+            "--master-addr=127.0.0.1", f"--master-port={_free_port()}"])
+    cmd = run + [str(HERE.parent / "bench.py"), "--gpus", "2",
+                 "--steps", str(steps), "--warmup", "2", "--cpu-baseline-s", "0", "--no-parity", "--no-decode-alone",
+                 "--host-e2e", "0", "--strict-steps", "2", "--dump-ids", str(dump)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["global_batch"] == 16
+    assert d["launch"]["world_size"] == 2 and d["launch"]["backend"] == "gloo"
+    assert d["launch"]["launcher"].startswith("bench.py --gpus" if launcher == "self" else "external")
     assert d["strict_batch"]["value"] > 0
     got = np.load(dump)
     assert got.shape == (2 * steps, 8, 24)

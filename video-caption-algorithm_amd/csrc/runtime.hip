@@ -175,7 +175,7 @@ struct DecBufs {
   int* finished;
   float* proc;        // [B][V] processed scores (sampling mode)
   unsigned* seed;     // [2] Philox key of the sampling draws
-  unsigned* persist;  // persistent decode: barrier words + device layer table
+  unsigned* arrive;   // [H] per-head arrival counters of the fused c_attn + attention launch
 };
 
 int max_logit_blocks(int V, int B) { return vcap_logit_blocks(V, B); }
@@ -197,8 +197,8 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.kc = c.take(per_layer * d->n_layer * es);
   b.vc = c.take(per_layer * d->n_layer * es);
   b.pt = (int*)c.take(pages * 4);
-  // argmax partials: the launch chain's lm_head blocks, or the persistent decode's <= 256 workgroups
-  const int nb = std::max(max_logit_blocks(d->vocab, B), 256);
+  // argmax partials: the lm_head's 64-column GEMV blocks or its stream kernel's grid (<= CUs)
+  const int nb = std::max({max_logit_blocks(d->vocab, B), vcap_device_cus(), 256});
   b.pval = (float*)c.take((size_t)B * nb * 4);
   b.pidx = (int*)c.take((size_t)B * nb * 4);
   b.hist = (int*)c.take((size_t)B * max_new * 4);
@@ -207,7 +207,7 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.finished = (int*)c.take((size_t)B * 4);
   b.proc = (float*)c.take((size_t)B * d->vocab * 4);
   b.seed = (unsigned*)c.take(8);
-  b.persist = (unsigned*)c.take(vcap_persist_ws_bytes());
+  b.arrive = (unsigned*)c.take(256 * 4);
   return b;
 }
 
@@ -228,8 +228,11 @@ int check_gpt2_launch(const vcap_gpt2_desc* d) {
   return 0;
 }
 
+// fuse_attn: run each layer's attention inside its c_attn launch where eligible (bf16, <= 16 rows,
+// one new position, context <= 64: vcap_qkv_attention_dispatch); needs w.arrive zeroed
+// (vcap_decode_init) - bit-identical to the two-launch form
 int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_elems, int M, int S_new, int past,
-               int max_blocks, hipStream_t s, const int* anc = nullptr, int anc_ld = 0) {
+               int max_blocks, hipStream_t s, const int* anc = nullptr, int anc_ld = 0, bool fuse_attn = false) {
   const int E = d->n_embd, H = d->n_head, L = d->n_layer;
   const int dt = d->dtype;
   const size_t es = esize(dt);
@@ -248,12 +251,17 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     // pages are allocated contiguously per sequence (identity table written by vcap_decode_init):
     // the scatter computes page ids instead of loading them (nullptr table)
     a.page_table = nullptr; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past; a.max_blocks = max_blocks;
-    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
+    a.arrive = w.arrive; a.attn_out = w.attn;
+    bool fused = false;
+    if (fuse_attn && dt == VCAP_DT_BF16 && !anc) VCAP_TRY(vcap_qkv_attention_dispatch(a, &fused, s), "c_attn+attention");
+    if (!fused) VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
     // 2) causal attention over the paged cache
     // pages are allocated contiguously per sequence (vcap_decode_init: identity table), so the bf16
     // short-context kernel computes page ids instead of loading them (nullptr table)
     const int* pt_arg = (dt == VCAP_DT_BF16 && past + S_new <= 64) ? nullptr : w.pt;
-    if (anc)   // beam search: keys through the ancestry table (one query row per sequence)
+    if (fused) {
+      // done inside the c_attn launch
+    } else if (anc)   // beam search: keys through the ancestry table (one query row per sequence)
       VCAP_TRY(vcap_decode_attention_anc_dispatch(dt, w.q, a.kc, a.vc, anc, anc_ld, maxp, w.attn, M, H, past, s),
                "decode_attention_anc");
     else
@@ -301,27 +309,6 @@ int run_lm_head(const vcap_gpt2_desc* d, const DecBufs& w, int rows, int S_new, 
   return 0;
 }
 
-// Workgroups of the persistent decode for this call, 0 = the launch chain.  gp->persistent: 0 off,
-// > 0 that many workgroups, < 0 auto (VCAP_PERSIST_G or 128).  Eligible: bf16, <= 16 rows, greedy
-// (no sampling), GPT-2 widths the kernel is instantiated for, at most one workgroup per CU.
-int persist_wgs(const vcap_gpt2_desc* d, const vcap_gen_params* gp, int B, int max_new, bool sampling) {
-  if (gp->persistent == 0 || sampling || d->dtype != VCAP_DT_BF16 || B > 16 || max_new < 2) return 0;
-  if (d->n_embd != 768 && d->n_embd != 1024 && d->n_embd != 128) return 0;
-  if (d->n_layer > kPersistMaxLayers) return 0;
-  int G = gp->persistent;
-  if (G < 0) {
-    static const int env = [] {
-      const char* e = std::getenv("VCAP_PERSIST_G");
-      return e ? (int)std::strtol(e, nullptr, 10) : 0;
-    }();
-    G = env > 0 ? env : 128;
-  }
-  G = std::max(G, vcap_persist_min_wgs(d->n_embd));
-  if (G > vcap_device_cus() || G > 256) return 0;
-  if ((d->vocab + 15) / 16 > 64 * G || B * d->n_head > 4 * G) return 0;
-  return G;
-}
-
 // sp != nullptr: sampling mode (HF _sample): the lm_head also stores the processed scores, the
 // sample kernel warps them and draws (or takes force_ids), and hands the token to the finalize kernel
 int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* ids, int nids,
@@ -331,38 +318,14 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
   const int E = d->n_embd, V = d->vocab;
   const int P = d->prefix_len, S0 = P + nids, max_new = gp->max_new_tokens;
   const int dt = d->dtype;
-  VCAP_TRY(vcap_decode_init_dispatch(w.pt, B, maxp, w.finished, w.nbanned, s), "decode_init");
+  VCAP_TRY(vcap_decode_init_dispatch(w.pt, B, maxp, w.finished, w.nbanned, s, w.arrive, d->n_head), "decode_init");
   VCAP_TRY(vcap_prefill_embed_dispatch(dt, prefix, P, ids, nids, d->wte, d->wpe, w.h, B, E, s), "prefill_embed");
-  const int G = persist_wgs(d, gp, B, max_new, sp != nullptr);
   for (int step = 0; step < max_new; ++step) {
-    if (G > 0 && step == 1) {
-      // steps 1 .. max_new-1: one persistent launch (csrc/decode_persist.hip), bit-identical
-      PersistDesc pd;
-      memset(&pd, 0, sizeof(pd));
-      pd.G = G; pd.M = B; pd.E = E; pd.H = d->n_head; pd.L = d->n_layer; pd.V = V; pd.S0 = S0; pd.maxp = maxp;
-      // (diagnostic: VCAP_PERSIST_STEPS=k runs steps 1 .. k-1 persistent and the rest as the chain)
-      static const int diag_steps = [] {
-        const char* e = std::getenv("VCAP_PERSIST_STEPS");
-        return e ? (int)std::strtol(e, nullptr, 10) : 0;
-      }();
-      const int step1 = diag_steps > 1 && diag_steps < max_new ? diag_steps : max_new;
-      pd.n_pos = d->n_positions; pd.step0 = 1; pd.step1 = step1; pd.ln_eps = d->ln_eps;
-      pd.lnf_g = d->lnf_g; pd.lnf_b = d->lnf_b; pd.lm_head = d->lm_head; pd.wte = d->wte; pd.wpe = d->wpe;
-      pd.h = w.h; pd.q = w.q; pd.attn = w.attn; pd.act = w.act; pd.kc = w.kc; pd.vc = w.vc;
-      pd.page_elems = (long)page_elems;
-      pd.hist = w.hist; pd.banned = w.banned; pd.nbanned = w.nbanned; pd.finished = w.finished;
-      pd.hist_ld = max_new; pd.ngram = gp->no_repeat_ngram_size; pd.rep = gp->repetition_penalty;
-      pd.min_new = gp->min_new_tokens; pd.eos = gp->eos_token_id; pd.pad = gp->pad_token_id;
-      pd.out_ids = out_ids; pd.out_ld = max_new; pd.logits_out = logits_out;
-      pd.pval = w.pval; pd.pidx = w.pidx; pd.bar = w.persist;
-      pd.layers = reinterpret_cast<const PersistLayer*>(d->layers);
-      VCAP_TRY(vcap_decode_persist_dispatch(pd, s), "decode_persist");
-      if (step1 == max_new) break;
-      step = step1;
-    }
     const int S_new = step == 0 ? S0 : 1;
     const int past = step == 0 ? 0 : S0 + step - 1;
-    if (int rc = run_layers(d, w, maxp, page_elems, B * S_new, S_new, past, gp->max_blocks, s)) return rc;
+    if (int rc = run_layers(d, w, maxp, page_elems, B * S_new, S_new, past, gp->max_blocks, s, nullptr, 0,
+                            !gp->split_attention))
+      return rc;
     int nblk = 0;
     if (int rc = run_lm_head(d, w, B, S_new, logits_out ? logits_out + (size_t)step * B * V : nullptr, max_new, step,
                              gp->repetition_penalty, gp->min_new_tokens, gp->eos_token_id, &nblk, s,
@@ -1195,7 +1158,6 @@ int vcap_decode_attention(int dtype, const void* q, const void* k_pool, const vo
   return 0;
 }
 
-unsigned vcap_decode_faults(void) { return vcap_decode_persist_faults(); }
 
 void vcap_graph_cache_clear(void) {
   std::vector<GraphEntry> evicted;

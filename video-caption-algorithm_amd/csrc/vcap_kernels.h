@@ -29,7 +29,9 @@ struct GemmEpi {
 enum { PRO_LN = 0, PRO_DIRECT = 1 };
 // EPI_LSE: raw logits -> logits_raw + per-workgroup (max, sum exp(x - max)) partials per row
 // (part_val / part_sum): the log_softmax statistics of beam search
-enum { EPI_QKV = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_LOGITS = 3, EPI_STORE = 4, EPI_LSE = 5 };
+// EPI_QKVA: EPI_QKV whose last workgroup to store a head's q / k / v columns then runs that head's
+// causal attention for all rows (decode.hip, vcap_qkv_attention_dispatch)
+enum { EPI_QKV = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_LOGITS = 3, EPI_STORE = 4, EPI_LSE = 5, EPI_QKVA = 6 };
 
 struct RowsGemmArgs {
   const void* x;  // PRO_LN: f32 residual rows; PRO_DIRECT: T rows
@@ -62,6 +64,9 @@ struct RowsGemmArgs {
   int min_new, eos;
   int max_blocks;  // 0: one 16-column tile per workgroup; > 0: widen tiles to stay near this grid
   float* proc_out;  // EPI_LOGITS, optional [M, N]: the processed scores (sampling mode)
+  // EPI_QKVA: per-head arrival counters (zero on entry, left zero) and the attention output T [M, E]
+  unsigned* arrive;
+  void* attn_out;
 };
 
 // ---- sampling warpers + draw (csrc/sample.hip)
@@ -124,7 +129,12 @@ hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc,
 hipError_t vcap_prefill_embed_dispatch(int dt, const float* prefix, int P, const int* ids, int nids, const void* wte,
                                        const float* wpe, float* h, int B, int E, hipStream_t s, int pos0 = 0,
                                        int prefix_rep = 1);
-hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s);
+hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s,
+                                     unsigned* arrive = nullptr, int n_arrive = 0);
+// ln_1 + c_attn + causal attention of a bf16 decode step (M <= 16 rows, one new position, context
+// <= 64, identity pages) as ONE launch; *done = false when the shape is not eligible (the caller
+// then runs vcap_rows_gemm_dispatch(EPI_QKV) + vcap_decode_attention_dispatch)
+hipError_t vcap_qkv_attention_dispatch(const RowsGemmArgs& a, bool* done, hipStream_t s);
 hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const int* part_idx, int nblk, int B,
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,
@@ -162,61 +172,6 @@ int vcap_beam_chunks(int V);
 hipError_t vcap_decode_attention_anc_dispatch(int dt, const void* q, const void* kc, const void* vc, const int* anc,
                                               int anc_ld, int maxp, void* out, int M, int H, int past,
                                               hipStream_t s);
-
-// ---- persistent greedy decode (csrc/decode_persist.hip): steps [step0, step1) of a bf16 decode of
-// M <= 16 rows as one launch of G workgroups (one per CU); state as the launch chain leaves it
-constexpr int kPersistMaxLayers = 24;
-struct PersistLayer {  // same field order as vcap_gpt2_layer (include/vcap.h)
-  const float* ln1_g;
-  const float* ln1_b;
-  const void* attn_w;
-  const float* attn_b;
-  const void* aproj_w;
-  const float* aproj_b;
-  const float* ln2_g;
-  const float* ln2_b;
-  const void* fc_w;
-  const float* fc_b;
-  const void* mproj_w;
-  const float* mproj_b;
-};
-struct PersistDesc {
-  int G, M, E, H, L, V, S0, maxp, n_pos;
-  int step0, step1;
-  float ln_eps;
-  const float* lnf_g;
-  const float* lnf_b;
-  const void* lm_head;
-  const void* wte;
-  const float* wpe;
-  float* h;
-  void* q;
-  void* attn;
-  void* act;
-  void* kc;
-  void* vc;
-  long page_elems;
-  int* hist;
-  int* banned;
-  int* nbanned;
-  int* finished;
-  int hist_ld;
-  int ngram;
-  float rep;
-  int min_new, eos, pad;
-  int* out_ids;
-  int out_ld;
-  float* logits_out;   // optional [hist_ld][M][V] (row block of step s at s * M * V)
-  float* pval;         // [M][G]
-  int* pidx;
-  unsigned* bar;       // vcap_persist_ws_bytes(): arrival counters (zeroed by the dispatch) + layer table
-  const PersistLayer* layers;
-};
-hipError_t vcap_decode_persist_dispatch(const PersistDesc& d, hipStream_t s);
-int vcap_persist_min_wgs(int E);
-size_t vcap_persist_bar_bytes();
-size_t vcap_persist_ws_bytes();   // at d.bar: barrier words, then the device layer table
-unsigned vcap_decode_persist_faults();
 
 hipError_t vcap_kv_gather_dispatch(int dt, const void* src_pool, void* dst_pool, const int* src_rows, int rows, int maxp,
                                    int H, int len, long layer_elems, int L, hipStream_t s);

@@ -16,7 +16,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
 DT_F32, DT_BF16, DT_MXFP8 = 0, 1, 2
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
@@ -63,7 +63,7 @@ class GPT2Desc(C.Structure):
 class GenParams(C.Structure):
     _fields_ = [("max_new_tokens", i32), ("min_new_tokens", i32), ("no_repeat_ngram_size", i32),
                 ("repetition_penalty", f32), ("eos_token_id", i32), ("pad_token_id", i32), ("use_graph", i32),
-                ("max_blocks", i32), ("persistent", i32)]
+                ("max_blocks", i32), ("split_attention", i32)]
 
 
 class BeamParams(C.Structure):
@@ -111,7 +111,6 @@ SIGNATURES = {
     "vcap_gpt2_sample": (i32, [C.POINTER(GPT2Desc), C.POINTER(GenParams), C.POINTER(SampleParams), vp,
                                C.POINTER(C.c_int), i32, i32, vp, vp, vp, vp, vp, sz, vp]),
     "vcap_graph_cache_clear": (None, []),
-    "vcap_decode_faults": (C.c_uint, []),
     "vcap_graph_cache_size": (i32, []),
     "vcap_gpt2_max_rows": (i32, []),
     "vcap_gpt2_beam_search_workspace_bytes": (sz, [C.POINTER(GPT2Desc), i32, i32, i32, i32]),

@@ -119,11 +119,6 @@ typedef struct vcap_gen_params {
   int max_blocks;            /* 0: whole-chip grids; > 0: cap the projection GEMV grids near this
                                 many workgroups (wider tiles per workgroup) - for a decode that
                                 shares the GPU with an encode holding most CUs */
-  int split_attention;       /* 0: bf16 decode steps of <= 16 rows run each layer's causal attention
-                                inside its c_attn launch (the last workgroup to store a head's
-                                q / k / v columns attends that head: one launch per layer fewer);
-                                1: c_attn and attention as two launches (same arithmetic, ids and
-                                logits bit-identical; A/B runs and tests) */
 } vcap_gen_params;
 
 const char* vcap_last_error(void);

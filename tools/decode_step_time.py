@@ -1,7 +1,7 @@
 """Per-token decode step cost (hipGraph, alone on the GPU) for the library named by VCAP_LIB
 (ablation builds).  Environment: B (sequences, default 8), GPT2 (arch, default gpt2), BEAMS
 (default 1 = HF-greedy graph; > 1 = the device beam search graph, preset "detailed" shape), CAP
-(decode grid cap), SPLIT (1 = attention as its own launch instead of inside c_attn)."""
+(decode grid cap)."""
 import os, sys, time
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
@@ -26,8 +26,7 @@ with torch.cuda.stream(s):
     for mx in (lo, hi):
         if beams == 1:
             cfg = GenConfig(mx, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, True,
-                            max_blocks=int(os.environ.get("CAP", "0")),
-                            split_attention=bool(int(os.environ.get("SPLIT", "0"))))
+                            max_blocks=int(os.environ.get("CAP", "0")))
             run = lambda: dec.generate_ids(pre, [ga.bos_token_id], cfg)
         else:
             run = lambda: search.beam_search_device(dec, pre, [ga.bos_token_id], num_beams=beams, max_new_tokens=mx,
@@ -41,6 +40,5 @@ with torch.cuda.stream(s):
             run()
         torch.cuda.synchronize()
         res[mx] = (time.perf_counter() - t) / 10 * 1e3
-print(f"{Path(os.environ.get('VCAP_LIB', 'base')).name} {name} B={B} beams={beams} cap={os.environ.get('CAP', '0')} "
-      f"split={os.environ.get('SPLIT', '0')}: "
+print(f"{Path(os.environ.get('VCAP_LIB', 'base')).name} {name} B={B} beams={beams} cap={os.environ.get('CAP', '0')}: "
       f"step {(res[hi]-res[lo])/(hi-lo)*1e3:.1f} us first {res[lo]*1e3:.0f} us")

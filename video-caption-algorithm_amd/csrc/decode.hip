@@ -211,39 +211,30 @@ constexpr bool gemv_stream_a() {
 // P.V with lane = (key group kg of 8, 8 consecutive dims d8), partial sums reduced over the 8 key
 // groups by DPP + permlane swaps.  c64_issue issues every load of the item at once (q, the lane's
 // K row, its 8 V rows: one memory round trip); c64_finish is the arithmetic, the ONE operation
-// order that vcap_decode_attention_c64_kernel and the fused c_attn + attention launch
-// (EPI_QKVA) share, so both give bit-identical outputs.  SC1: write-through-coherent buffer loads
-// (`sc1`), for bytes another workgroup of the same launch stored `sc1` (MI355X_MICROARCH.md,
-// valid hand-off forms); otherwise plain loads of bytes an earlier launch wrote.
+// order of vcap_decode_attention_c64_kernel.
 struct C64Loads {
   u32x4 q;      // 8 of the head's 64 query dims: chunk (lane & 7)
   u32x4 kv[8];  // K row of key min(lane, ctx - 1)
   u32x4 vv[8];  // V rows of keys it * 8 + kg (clamped), dims [d8, d8 + 8)
 };
 
-template <bool SC1>
-VCAP_DEV u32x4 c64_ld16(const bf16_t* base, long elem) {
-  if constexpr (SC1) return vcap_buf_load16<16>(base, elem * 2);
-  else return *reinterpret_cast<const u32x4*>(base + elem);
-}
+VCAP_DEV u32x4 c64_ld16(const bf16_t* base, long elem) { return *reinterpret_cast<const u32x4*>(base + elem); }
 
-template <bool SC1>
 VCAP_DEV void c64_issue(C64Loads& L, const bf16_t* q, const bf16_t* kc, const bf16_t* vc, int maxp, int m, int h,
                         int H, int seq, int ctx) {
   const int lane = threadIdx.x & 63, kg = lane >> 3, d8 = (lane & 7) * 8;
   auto row_of = [&](int j) { return (((long)(seq * maxp + (j >> 4)) * H + h) * 16 + (j & 15)) * 64; };
-  L.q = c64_ld16<SC1>(q, (long)m * H * 64 + h * 64 + (lane & 7) * 8);
+  L.q = c64_ld16(q, (long)m * H * 64 + h * 64 + (lane & 7) * 8);
   const long kr = row_of(min(lane, ctx - 1));
 #pragma unroll
-  for (int c = 0; c < 8; ++c) L.kv[c] = c64_ld16<SC1>(kc, kr + c * 8);
+  for (int c = 0; c < 8; ++c) L.kv[c] = c64_ld16(kc, kr + c * 8);
 #pragma unroll
-  for (int it = 0; it < 8; ++it) L.vv[it] = c64_ld16<SC1>(vc, row_of(min(it * 8 + kg, ctx - 1)) + d8);
+  for (int it = 0; it < 8; ++it) L.vv[it] = c64_ld16(vc, row_of(min(it * 8 + kg, ctx - 1)) + d8);
 }
 
 // s_q / s_p: this wave's 64 floats each of LDS; orow = out + m * E + h * 64
-VCAP_DEV void c64_finish(const C64Loads& L, float* s_q, float* s_p, int ctx, bf16_t* orow, bool store = true) {
+VCAP_DEV void c64_finish(const C64Loads& L, float* s_q, float* s_p, int ctx, bf16_t* orow) {
   const int lane = threadIdx.x & 63, kg = lane >> 3, d8 = (lane & 7) * 8;
-  __builtin_amdgcn_wave_barrier();  // the previous item's reads of s_q / s_p are done
   if (lane < 8) {
     const unsigned w4[4] = {L.q.x, L.q.y, L.q.z, L.q.w};
 #pragma unroll
@@ -283,98 +274,12 @@ VCAP_DEV void c64_finish(const C64Loads& L, float* s_q, float* s_p, int ctx, bf1
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = rows_sum(o[e] + dpp_f<0x128>(o[e]));
-  if (kg == 0 && store) {
+  if (kg == 0) {
     const float inv = 1.0f / sum;
     *reinterpret_cast<u32x4*>(orow + d8) =
         (u32x4){pack_bf2(o[0] * inv, o[1] * inv), pack_bf2(o[2] * inv, o[3] * inv),
                 pack_bf2(o[4] * inv, o[5] * inv), pack_bf2(o[6] * inv, o[7] * inv)};
   }
-}
-
-// ------------------------------------------------------------------------------------------------
-// EPI_QKVA epilogue (bf16, M <= 16 rows of one new position each, identity pages): the c_attn
-// outputs of this workgroup's NTB tiles - all inside one 64-column head group of q, k or v - go
-// out as one 16-byte write-through (`sc1`) store per lane (8 consecutive columns; the same sums
-// and rounding as EPI_QKV's element stores), every storing wave drains them (vmcnt(0)), the
-// workgroup meets, and one lane adds 1 to the head's arrival counter.  The workgroup whose add
-// completes the head (3 x 64 / (16 NTB) arrivals) attends that head for all M rows, reading the
-// handed-off q / k / v with `sc1` loads - the MI355X guide's valid hand-off form "one lane of each
-// storing workgroup adds to one unsharded counter; the workgroup whose add came last loads after
-// its add returned, the other waves after a workgroup barrier" - and resets the counter for the
-// next launch.  No workgroup waits on another, so residency and dispatch order do not matter.
-// Rows are spread over the 4 waves (row wave + 4k), the next row's loads issued before the
-// current row's arithmetic.
-// NI rows of head h per wave (rows wave + 4i, clamped to M - 1: a clamped duplicate is computed
-// and not stored), row i + 1's loads issued before row i's arithmetic
-template <int NI>
-VCAP_DEV void qkv_attention_rows(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, bf16_t* out, int maxp, int h,
-                                 int H, int ctx, int M, float* s_q, float* s_p) {
-  const int wave = threadIdx.x >> 6, E = H * 64;
-  C64Loads L[2];
-  c64_issue<true>(L[0], q, kc, vc, maxp, min(wave, M - 1), h, H, min(wave, M - 1), ctx);
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int m = wave + 4 * i, mn = min(m + 4, M - 1);
-    if (i + 1 < NI) c64_issue<true>(L[(i + 1) & 1], q, kc, vc, maxp, mn, h, H, mn, ctx);
-    c64_finish(L[i & 1], s_q, s_p, ctx, out + (long)min(m, M - 1) * E + h * 64, m < M);
-  }
-}
-
-template <int NTB>
-VCAP_DEV void qkv_attention_tail(const RowsGemmArgs& a, const float (*red)[NTB * 256], const f32x4 (&qb)[2],
-                                 float* s_att, int& s_head, int n0) {
-  const int tid = threadIdx.x, wave = tid >> 6;
-  const int M = a.M, Ed = a.N / 3, H = a.H;
-  if (tid < NTB * 32) {
-    const int j = tid >> 5, r = (tid >> 1) & 15, c8 = (tid & 1) * 8;
-    const int n = n0 + j * 16 + c8;
-    if (r < M) {
-      float v[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const int e = j * 256 + r * 16 + c8 + c;
-        v[c] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]) + (c < 4 ? qb[0][c] : qb[1][c - 4]);
-      }
-      const u32x4 pk = (u32x4){pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
-      const int which = n / Ed, within_e = n - which * Ed;
-      if (which == 0) {
-        __builtin_amdgcn_raw_buffer_store_b128(pk, __builtin_amdgcn_make_buffer_rsrc(a.q_out, 0, 0x7FFFFFFF, 0x00020000),
-                                               ((long)r * Ed + within_e) * 2, 0, 16);
-      } else {
-        const int head = within_e >> 6, d = within_e & 63, pos = a.past;
-        const long el = (((long)(r * a.maxp + (pos >> 4)) * H + head) * 16 + (pos & 15)) * 64 + d;
-        __builtin_amdgcn_raw_buffer_store_b128(pk, __builtin_amdgcn_make_buffer_rsrc(which == 1 ? a.kc : a.vc, 0,
-                                                                                     0x7FFFFFFF, 0x00020000),
-                                               el * 2, 0, 16);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
-  __syncthreads();
-  if (tid == 0) {
-    const int head = (n0 % Ed) >> 6, arrivals = 3 * (64 / (16 * NTB));
-    const unsigned old = __hip_atomic_fetch_add(a.arrive + head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_head = old == (unsigned)(arrivals - 1) ? head : -1;
-    if (old == (unsigned)(arrivals - 1)) __hip_atomic_store(a.arrive + head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const int h = s_head;
-  if (h < 0) return;
-  const bf16_t* q = (const bf16_t*)a.q_out;
-  const bf16_t* kc = (const bf16_t*)a.kc;
-  const bf16_t* vc = (const bf16_t*)a.vc;
-  bf16_t* out = (bf16_t*)a.attn_out;
-  const int ctx = a.past + 1;
-  float* s_q = s_att + wave * 64;
-  float* s_p = s_att + 256 + wave * 64;
-  // rows wave, wave + 4, ... (M <= 16): straight-line code per rows-per-wave count, so the
-  // compiler's waits stay counted (a branch between a row's loads and its arithmetic makes it
-  // drain every load in flight at the join)
-  const int per = (M + 3) >> 2;
-  if (per == 1) qkv_attention_rows<1>(q, kc, vc, out, a.maxp, h, H, ctx, M, s_q, s_p);
-  else if (per == 2) qkv_attention_rows<2>(q, kc, vc, out, a.maxp, h, H, ctx, M, s_q, s_p);
-  else if (per == 3) qkv_attention_rows<3>(q, kc, vc, out, a.maxp, h, H, ctx, M, s_q, s_p);
-  else qkv_attention_rows<4>(q, kc, vc, out, a.maxp, h, H, ctx, M, s_q, s_p);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -397,8 +302,6 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   __shared__ __attribute__((aligned(16))) float red[4][NE * 256];
   __shared__ float lg[LGM][NTB * 16];
   __shared__ unsigned char s_rep[LGM][NTB * 16], s_ban[LGM][NTB * 16];
-  __shared__ float s_att[EPI == EPI_QKVA ? 2 * 4 * 64 : 1];  // EPI_QKVA: per wave 64 q + 64 p floats
-  __shared__ int s_head;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
@@ -466,14 +369,6 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   }
   ProcToks<EPI == EPI_LOGITS ? MT : 1> toks;
   if constexpr (EPI == EPI_LOGITS) toks.load(a, m0);
-  // EPI_QKVA: the bias of the 8 consecutive columns this lane stores (tile tid >> 5, row
-  // (tid >> 1) & 15, columns (tid & 1) * 8 ..)
-  f32x4 qb[EPI == EPI_QKVA ? 2 : 1];
-  if constexpr (EPI == EPI_QKVA) {
-    const int nb = min(n0 + ((tid >> 5) % NTB) * 16 + (tid & 1) * 8, N - 8);
-    qb[0] = *reinterpret_cast<const f32x4*>(a.bias + nb);
-    qb[1] = *reinterpret_cast<const f32x4*>(a.bias + nb + 4);
-  }
   // Issue order fence: every load above is issued before any of the work below.  The empty asm
   // statements take the first-consumed operands as in/out registers and clobber memory, so no
   // load sinks below them and no LayerNorm arithmetic / MFMA chain is hoisted above them (the
@@ -565,11 +460,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
       for (int r = 0; r < 4; ++r) red[wave][(i * NTB + j) * 256 + (fg * 4 + r) * 16 + fr] = acc[i][j][r];
   if constexpr (EPI == EPI_LOGITS) toks.template mark<NTB>(a, m0, n0, s_rep, s_ban);
   __syncthreads();
-  if constexpr (EPI == EPI_QKVA) {
-    qkv_attention_tail<NTB>(a, red, qb, s_att, s_head, n0);
-  } else {
-    rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0);
-  }
+  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -898,15 +789,13 @@ __global__ __launch_bounds__(256) void vcap_kv_gather_kernel(const T* __restrict
 }
 
 // Per-step state init: identity page tables, cleared history / flags.
-__global__ void vcap_decode_init_kernel(int* page_table, int B, int maxp, int* finished, int* nbanned,
-                                        unsigned* arrive, int n_arrive) {
+__global__ void vcap_decode_init_kernel(int* page_table, int B, int maxp, int* finished, int* nbanned) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < B * maxp) page_table[i] = i;
   if (i < B) {
     finished[i] = 0;
     nbanned[i] = 0;
   }
-  if (i < n_arrive) arrive[i] = 0u;  // EPI_QKVA counters (each launch leaves them zero again)
 }
 
 // Reduce the per-workgroup argmax partials, apply EOS padding, record the token, precompute the
@@ -1304,25 +1193,6 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
   return hipErrorInvalidValue;
 }
 
-hipError_t vcap_qkv_attention_dispatch(const RowsGemmArgs& a, bool* done, hipStream_t s) {
-  *done = false;
-  const int E = a.N / 3;
-  if (a.M > 16 || a.M <= 0 || a.S_new != 1 || a.past + 1 > 64 || a.page_table || !a.arrive || !a.attn_out ||
-      a.N != 3 * a.K || E != a.H * 64 || a.H > 256 || (a.K != 768 && a.K != 1024))
-    return hipSuccess;
-  if ((long)a.M * a.ldx * 4 >= 0x7FFFFFFFL) return hipSuccess;
-  const int ntb = rows_ntb(EPI_QKV, a.N, a.max_blocks);
-  *done = true;
-#define VCAP_QKVA(NT)                                                                              \
-  if (ntb == NT)                                                                                    \
-    return a.K == 768 ? launch_gemv<bf16_t, 1, NT, PRO_LN, EPI_QKVA, 6>(a, s)                      \
-                      : launch_gemv<bf16_t, 1, NT, PRO_LN, EPI_QKVA, 8>(a, s);
-  VCAP_QKVA(1) VCAP_QKVA(2) VCAP_QKVA(4)
-#undef VCAP_QKVA
-  *done = false;
-  return hipSuccess;
-}
-
 hipError_t vcap_rows_pack_dispatch(int dt, const void* w, long ldw, int N, int K, void* packed, hipStream_t s) {
   const int ks = dt == VCAP_DT_BF16 ? 32 : 16;
   const size_t esz = dt == VCAP_DT_BF16 ? 2 : 4;
@@ -1362,7 +1232,7 @@ __global__ __launch_bounds__(64) void vcap_decode_attention_c64_kernel(const bf1
   const int seq = m / S_new, qpos = past + (m - seq * S_new);
   const int ctx = qpos + 1;  // <= 64 (dispatcher)
   C64Loads L;
-  c64_issue<false>(L, q, kc, vc, maxp, m, h, H, seq, ctx);
+  c64_issue(L, q, kc, vc, maxp, m, h, H, seq, ctx);
   c64_finish(L, s_q, s_p, ctx, out + (long)m * H * 64 + h * 64);
 }
 
@@ -1426,11 +1296,10 @@ hipError_t vcap_kv_gather_dispatch(int dt, const void* src_pool, void* dst_pool,
   return hipGetLastError();
 }
 
-hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s,
-                                     unsigned* arrive, int n_arrive) {
-  const int n = std::max(std::max(B * maxp, B), arrive ? n_arrive : 0);
+hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s) {
+  const int n = std::max(B * maxp, B);
   hipLaunchKernelGGL(vcap_decode_init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, page_table, B, maxp, finished,
-                     nbanned, arrive, arrive ? n_arrive : 0);
+                     nbanned);
   return hipGetLastError();
 }
 

@@ -539,21 +539,14 @@ static hipError_t launch256_epi(const void* A, long lda, const void* W, long ldw
     // L2 beside its A panels (ViT-B: 12 x 384 KB): the widest group of whole tile columns dividing
     // tiles_n with <= 2.5 MB of weights, so an XCD keeps its group's tiles across rounds.  Measured
     // (profiles/r04_gemm_colgroup_ab.txt, 16-video fc1): FETCH 426 -> 294 MB per launch, 310 -> 306 us
-    // in the pipelined bench, equal alone.  VCAP_GEMM_COLGROUP=w overrides (0: row-major).
-    static const int env_w = [] {
-      const char* v = std::getenv("VCAP_GEMM_COLGROUP");
-      return v ? (int)std::strtol(v, nullptr, 10) : -1;
-    }();
-    int w = env_w;
-    if (w < 0) {
-      const long tile_bytes = (long)TN * K * (long)sizeof(TIn);
-      w = 0;
-      for (int c = tiles_n - 1; c >= 1; --c)
-        if (tiles_n % c == 0 && c * tile_bytes <= 2560L * 1024) {
-          w = c;
-          break;
-        }
-    }
+    // in the pipelined bench, equal alone.
+    const long tile_bytes = (long)TN * K * (long)sizeof(TIn);
+    int w = 0;
+    for (int c = tiles_n - 1; c >= 1; --c)
+      if (tiles_n % c == 0 && c * tile_bytes <= 2560L * 1024) {
+        w = c;
+        break;
+      }
     if (w > 0 && w < tiles_n && tiles_n % w == 0) e.colgroup = w;
   }
   hipLaunchKernelGGL((vcap_gemm256_kernel<TIn, TOut, EPI>), dim3(tiles), dim3(512), lds, s, (const TIn*)A, lda,

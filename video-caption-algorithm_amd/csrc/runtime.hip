@@ -175,7 +175,6 @@ struct DecBufs {
   int* finished;
   float* proc;        // [B][V] processed scores (sampling mode)
   unsigned* seed;     // [2] Philox key of the sampling draws
-  unsigned* arrive;   // [H] per-head arrival counters of the fused c_attn + attention launch
 };
 
 int max_logit_blocks(int V, int B) { return vcap_logit_blocks(V, B); }
@@ -207,7 +206,6 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.finished = (int*)c.take((size_t)B * 4);
   b.proc = (float*)c.take((size_t)B * d->vocab * 4);
   b.seed = (unsigned*)c.take(8);
-  b.arrive = (unsigned*)c.take(256 * 4);
   return b;
 }
 
@@ -228,11 +226,8 @@ int check_gpt2_launch(const vcap_gpt2_desc* d) {
   return 0;
 }
 
-// fuse_attn: run each layer's attention inside its c_attn launch where eligible (bf16, <= 16 rows,
-// one new position, context <= 64: vcap_qkv_attention_dispatch); needs w.arrive zeroed
-// (vcap_decode_init) - bit-identical to the two-launch form
 int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_elems, int M, int S_new, int past,
-               int max_blocks, hipStream_t s, const int* anc = nullptr, int anc_ld = 0, bool fuse_attn = false) {
+               int max_blocks, hipStream_t s, const int* anc = nullptr, int anc_ld = 0) {
   const int E = d->n_embd, H = d->n_head, L = d->n_layer;
   const int dt = d->dtype;
   const size_t es = esize(dt);
@@ -251,17 +246,12 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     // pages are allocated contiguously per sequence (identity table written by vcap_decode_init):
     // the scatter computes page ids instead of loading them (nullptr table)
     a.page_table = nullptr; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past; a.max_blocks = max_blocks;
-    a.arrive = w.arrive; a.attn_out = w.attn;
-    bool fused = false;
-    if (fuse_attn && dt == VCAP_DT_BF16 && !anc) VCAP_TRY(vcap_qkv_attention_dispatch(a, &fused, s), "c_attn+attention");
-    if (!fused) VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
+    VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
     // 2) causal attention over the paged cache
     // pages are allocated contiguously per sequence (vcap_decode_init: identity table), so the bf16
     // short-context kernel computes page ids instead of loading them (nullptr table)
     const int* pt_arg = (dt == VCAP_DT_BF16 && past + S_new <= 64) ? nullptr : w.pt;
-    if (fused) {
-      // done inside the c_attn launch
-    } else if (anc)   // beam search: keys through the ancestry table (one query row per sequence)
+    if (anc)   // beam search: keys through the ancestry table (one query row per sequence)
       VCAP_TRY(vcap_decode_attention_anc_dispatch(dt, w.q, a.kc, a.vc, anc, anc_ld, maxp, w.attn, M, H, past, s),
                "decode_attention_anc");
     else
@@ -318,14 +308,12 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
   const int E = d->n_embd, V = d->vocab;
   const int P = d->prefix_len, S0 = P + nids, max_new = gp->max_new_tokens;
   const int dt = d->dtype;
-  VCAP_TRY(vcap_decode_init_dispatch(w.pt, B, maxp, w.finished, w.nbanned, s, w.arrive, d->n_head), "decode_init");
+  VCAP_TRY(vcap_decode_init_dispatch(w.pt, B, maxp, w.finished, w.nbanned, s), "decode_init");
   VCAP_TRY(vcap_prefill_embed_dispatch(dt, prefix, P, ids, nids, d->wte, d->wpe, w.h, B, E, s), "prefill_embed");
   for (int step = 0; step < max_new; ++step) {
     const int S_new = step == 0 ? S0 : 1;
     const int past = step == 0 ? 0 : S0 + step - 1;
-    if (int rc = run_layers(d, w, maxp, page_elems, B * S_new, S_new, past, gp->max_blocks, s, nullptr, 0,
-                            !gp->split_attention))
-      return rc;
+    if (int rc = run_layers(d, w, maxp, page_elems, B * S_new, S_new, past, gp->max_blocks, s)) return rc;
     int nblk = 0;
     if (int rc = run_lm_head(d, w, B, S_new, logits_out ? logits_out + (size_t)step * B * V : nullptr, max_new, step,
                              gp->repetition_penalty, gp->min_new_tokens, gp->eos_token_id, &nblk, s,

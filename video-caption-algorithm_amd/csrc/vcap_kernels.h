@@ -29,9 +29,7 @@ struct GemmEpi {
 enum { PRO_LN = 0, PRO_DIRECT = 1 };
 // EPI_LSE: raw logits -> logits_raw + per-workgroup (max, sum exp(x - max)) partials per row
 // (part_val / part_sum): the log_softmax statistics of beam search
-// EPI_QKVA: EPI_QKV whose last workgroup to store a head's q / k / v columns then runs that head's
-// causal attention for all rows (decode.hip, vcap_qkv_attention_dispatch)
-enum { EPI_QKV = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_LOGITS = 3, EPI_STORE = 4, EPI_LSE = 5, EPI_QKVA = 6 };
+enum { EPI_QKV = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_LOGITS = 3, EPI_STORE = 4, EPI_LSE = 5 };
 
 struct RowsGemmArgs {
   const void* x;  // PRO_LN: f32 residual rows; PRO_DIRECT: T rows
@@ -64,9 +62,6 @@ struct RowsGemmArgs {
   int min_new, eos;
   int max_blocks;  // 0: one 16-column tile per workgroup; > 0: widen tiles to stay near this grid
   float* proc_out;  // EPI_LOGITS, optional [M, N]: the processed scores (sampling mode)
-  // EPI_QKVA: per-head arrival counters (zero on entry, left zero) and the attention output T [M, E]
-  unsigned* arrive;
-  void* attn_out;
 };
 
 // ---- sampling warpers + draw (csrc/sample.hip)
@@ -129,12 +124,7 @@ hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc,
 hipError_t vcap_prefill_embed_dispatch(int dt, const float* prefix, int P, const int* ids, int nids, const void* wte,
                                        const float* wpe, float* h, int B, int E, hipStream_t s, int pos0 = 0,
                                        int prefix_rep = 1);
-hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s,
-                                     unsigned* arrive = nullptr, int n_arrive = 0);
-// ln_1 + c_attn + causal attention of a bf16 decode step (M <= 16 rows, one new position, context
-// <= 64, identity pages) as ONE launch; *done = false when the shape is not eligible (the caller
-// then runs vcap_rows_gemm_dispatch(EPI_QKV) + vcap_decode_attention_dispatch)
-hipError_t vcap_qkv_attention_dispatch(const RowsGemmArgs& a, bool* done, hipStream_t s);
+hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s);
 hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const int* part_idx, int nblk, int B,
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,

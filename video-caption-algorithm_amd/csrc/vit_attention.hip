@@ -276,106 +276,6 @@ VCAP_DEV void attn_bf16_qtile(const char* Ks, const char* Vs, const u32x4 (&qf)[
   inv = __builtin_amdgcn_rcpf(sum);
 }
 
-// Software-pipelined form (VCAP_ATTN_VARIANT=pipe, measured against the shipped kernel - DESIGN
-// §4 ViT attention): an online softmax over 32-key chunks in which chunk c + 1's S MFMAs are issued
-// ahead of chunk c's max / exp / rescale VALU and chunk c's PV MFMAs, so one wave's instruction
-// stream carries matrix and vector work together (two chunks of scores live instead of a whole
-// 208-key row).  Same operands, swizzles and row-sum-by-MFMA as attn_bf16_qtile.
-template <int KT, int KE>
-VCAP_DEV void attn_bf16_qtile_pipe(const char* Ks, const char* Vs, const u32x4 (&qf)[2], int N, f32x4 (&o)[4],
-                                   float& inv) {
-  const int lane = threadIdx.x & 63;
-  const int fr = lane & 15, fg = lane >> 4;
-  const float c2 = 0.125f * 1.4426950408889634f;
-  constexpr int NC = KT / 2;
-  auto s_chunk = [&](int c, f32x4 (&s)[2]) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kt = 2 * c + j;
-      f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-      if (kt < KE) {
-        const int key = kt * 16 + fr;
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-          const u32x4 kf = *reinterpret_cast<const u32x4*>(Ks + key * 128 + (((sl * 4 + fg) ^ (key & 7)) << 4));
-          acc = mfma_frag(kf, qf[sl], acc, (bf16_t*)nullptr);
-        }
-      }
-      s[j] = acc;
-    }
-  };
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 osum = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const u32x4 ones = (u32x4){0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
-  const int qr = fr >> 2, p4 = fr & 3;
-  float m = -INFINITY;
-  f32x4 sc[2], sn[2];
-  s_chunk(0, sc);
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    if (c + 1 < NC) s_chunk(c + 1, sn);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kt = 2 * c + j;
-      if (kt >= KE) {
-        sc[j] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-      } else if (kt >= KT - 2) {
-        const int lim = N - kt * 16 - fg * 4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sc[j][r] = r < lim ? sc[j][r] : -INFINITY;
-      }
-    }
-    float cm = fmaxf(max3f(sc[0][0], sc[0][1], sc[0][2]), max3f(sc[0][3], sc[1][0], sc[1][1]));
-    cm = max3f(cm, sc[1][2], sc[1][3]);
-    cm = rows_max(cm);
-    const float mn = fmaxf(m, cm);
-    const float alpha = __builtin_amdgcn_exp2f((m - mn) * c2);  // chunk 0: exp2(-inf) = 0
-    m = mn;
-    const float mc = mn * c2;
-    float p[8];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) p[4 * j + r] = __builtin_amdgcn_exp2f(fmaf(sc[j][r], c2, -mc));
-    const u32x4 pf = (u32x4){cvt_pk_bf16(p[0], p[1]), cvt_pk_bf16(p[2], p[3]), cvt_pk_bf16(p[4], p[5]),
-                             cvt_pk_bf16(p[6], p[7])};
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] = o[dt] * alpha;
-    osum = osum * alpha;
-    const int r0 = 32 * c + 4 * fg + qr, r1 = r0 + 16;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int ch = 2 * dt + (p4 >> 1);
-      const u32x2 lo = tr_read(Vs + r0 * 128 + ((ch ^ (r0 & 7)) << 4) + 8 * (p4 & 1));
-      const u32x2 hi = (KE < KT && c == NC - 1) ? (u32x2){0u, 0u}
-                                               : tr_read(Vs + r1 * 128 + ((ch ^ (r1 & 7)) << 4) + 8 * (p4 & 1));
-      o[dt] = mfma_frag((u32x4){lo.x, lo.y, hi.x, hi.y}, pf, o[dt], (bf16_t*)nullptr);
-    }
-    osum = mfma_frag(ones, pf, osum, (bf16_t*)nullptr);
-    if (c + 1 < NC) {
-      sc[0] = sn[0];
-      sc[1] = sn[1];
-    }
-    // hand-ordered stream for this chunk: the K fragment reads of chunk c + 1, then its 4 S MFMAs
-    // each followed by a run of chunk c's softmax VALU, then the V transpose reads and the 5 PV
-    // MFMAs interleaved with the rescale (masks: 0x8 MFMA, 0x2 VALU, 0x100 DS read)
-    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x2, 10, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x2, 4, 0);
-    }
-  }
-  inv = __builtin_amdgcn_rcpf(osum[0]);
-}
-
 // A query tile's output, packed for its stores: bf16 -> two dwordx4 per lane (lane pair exchange),
 // MXFP8 -> one dwordx4 per lane + the lane group 0 scale bytes.  Built right after the compute;
 // `attn_commit` stores it.
@@ -458,7 +358,7 @@ VCAP_DEV void attn_commit(const AttnOut& r, void* out, int D, int h, uint8_t* os
 // 39.1-39.7 vs 37.8-38.6 us at 128 frames, r03 (profiles/r03_attention_v_overlap_ab.txt): reverted.)
 // MXO: write the output as MXFP8 (e4m3 + E8M0 per 32 of the head's 64 dims) for an MXFP8 attn-proj
 // GEMM; oscale in the vcap_common.h layout over `groups` 256-row groups.
-template <int KT, int KE, int WAVES, bool MXO, bool PIPE = false>
+template <int KT, int KE, int WAVES, bool MXO>
 __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(const bf16_t* __restrict__ qkv,
                                                                              void* __restrict__ out, int N, int H,
                                                                              uint8_t* __restrict__ oscale,
@@ -507,11 +407,7 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
     if (qt >= qtiles) break;
     f32x4 o[4];
     float inv;
-    if constexpr (PIPE) {
-      attn_bf16_qtile_pipe<KT, KE>(Ks, Vs, qf[i], N, o, inv);
-    } else {
-      attn_bf16_qtile<KT, KE>(Ks, Vs, qf[i], N, o, inv);
-    }
+    attn_bf16_qtile<KT, KE>(Ks, Vs, qf[i], N, o, inv);
     const int q = qt * 16 + fr;
     const bool keep = q < N && (!cls_only || q == 0);
     const long row = cls_only ? (long)bt : (long)bt * N + q;
@@ -519,19 +415,19 @@ __global__ __launch_bounds__(WAVES * 64) void vcap_vit_attention_bf16_kernel(con
   }
 }
 
-template <int KT, int KE, int WAVES, bool MXO, bool PIPE = false>
+template <int KT, int KE, int WAVES, bool MXO>
 static hipError_t launch_attn_bf16(const void* qkv, void* out, int BT, int N, int H, uint8_t* oscale, int cls_only,
                                    hipStream_t s) {
   const size_t lds = (size_t)KE * 16 * 128 * 2;  // 53 KiB at KE = 13: three workgroups per CU
   static bool configured = false;
   if (!configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_bf16_kernel<KT, KE, WAVES, MXO, PIPE>,
+    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_attention_bf16_kernel<KT, KE, WAVES, MXO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     configured = true;
   }
   const int groups = ((cls_only ? BT : BT * N) + 255) / 256;  // scale rows = output rows
-  hipLaunchKernelGGL((vcap_vit_attention_bf16_kernel<KT, KE, WAVES, MXO, PIPE>), dim3(BT * H), dim3(WAVES * 64), lds, s,
+  hipLaunchKernelGGL((vcap_vit_attention_bf16_kernel<KT, KE, WAVES, MXO>), dim3(BT * H), dim3(WAVES * 64), lds, s,
                      (const bf16_t*)qkv, out, N, H, oscale, groups, cls_only);
   return hipGetLastError();
 }
@@ -560,15 +456,7 @@ static hipError_t attn_bf16_dispatch(const void* qkv, void* out, uint8_t* oscale
   switch (((N + 31) / 32) * 2) {  // keys padded to a multiple of 32
     case 2: return launch_attn_bf16<2, 2, 4, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
     case 14:
-      if (N <= 13 * 16) {
-        // diagnostic: VCAP_ATTN_VARIANT=pipe selects the software-pipelined online-softmax form
-        static const bool pipe = [] {
-          const char* e = std::getenv("VCAP_ATTN_VARIANT");
-          return e && std::strcmp(e, "pipe") == 0;
-        }();
-        if (pipe && !MXO) return launch_attn_bf16<14, 13, 8, false, true>(qkv, out, BT, N, H, oscale, cls_only, s);
-        return launch_attn_bf16<14, 13, 8, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
-      }
+      if (N <= 13 * 16) return launch_attn_bf16<14, 13, 8, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
       return launch_attn_bf16<14, 14, 8, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);
     case 18:
       if (N <= 17 * 16) return launch_attn_bf16<18, 17, 8, MXO>(qkv, out, BT, N, H, oscale, cls_only, s);

@@ -63,7 +63,7 @@ class GPT2Desc(C.Structure):
 class GenParams(C.Structure):
     _fields_ = [("max_new_tokens", i32), ("min_new_tokens", i32), ("no_repeat_ngram_size", i32),
                 ("repetition_penalty", f32), ("eos_token_id", i32), ("pad_token_id", i32), ("use_graph", i32),
-                ("max_blocks", i32), ("split_attention", i32)]
+                ("max_blocks", i32)]
 
 
 class BeamParams(C.Structure):

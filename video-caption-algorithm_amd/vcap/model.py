@@ -219,9 +219,6 @@ class GenConfig:
     top_k: int = 50
     top_p: float = 1.0
     seed: int = 0
-    # True: each layer's decode attention as its own launch after c_attn (A/B runs and tests); the
-    # default runs it inside the c_attn launch where eligible (bf16, <= 16 rows; bit-identical)
-    split_attention: bool = False
 
     @property
     def do_sample(self) -> bool:
@@ -340,7 +337,7 @@ class HipGPT2Decoder:
                          no_repeat_ngram_size=int(cfg.no_repeat_ngram_size),
                          repetition_penalty=float(cfg.repetition_penalty), eos_token_id=int(cfg.eos_token_id),
                          pad_token_id=int(cfg.pad_token_id), use_graph=int(bool(cfg.use_graph)),
-                         max_blocks=int(cfg.max_blocks), split_attention=int(bool(cfg.split_attention)))
+                         max_blocks=int(cfg.max_blocks))
         arr = (C.c_int * max(len(ids), 1))(*ids)
         ws = (workspace or self.ws).get(self.workspace_bytes(B, len(ids), mx))
         if cfg.do_sample:

@@ -30,6 +30,7 @@ from __future__ import annotations
 
 from typing import List, Optional, Sequence
 
+import atexit
 import ctypes as C
 
 import torch
@@ -48,8 +49,14 @@ from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, _Workspa
 _STREAM_SETS: dict = {}
 
 
+def _device_index(device) -> int:
+    d = torch.device(device)
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
 def _stream_set(device, reserve_cus: int, confine_decode: bool, lanes: int):
-    key = (torch.device(device).index or 0, reserve_cus, confine_decode and reserve_cus > 0, lanes)
+    device = torch.device("cuda", _device_index(device))   # 'cuda' = the current device, resolved once
+    key = (device.index, reserve_cus, confine_decode and reserve_cus > 0, lanes)
     if key in _STREAM_SETS:
         return _STREAM_SETS[key][:2]
     lo, hi = torch.cuda.Stream.priority_range()
@@ -85,7 +92,8 @@ def _stream_set(device, reserve_cus: int, confine_decode: bool, lanes: int):
 
 
 def release_streams() -> None:
-    """Destroy the CU-masked streams of every cached stream set (after all pipelines are closed)."""
+    """Destroy the CU-masked streams of every cached stream set (after all pipelines are closed).
+    Registered with atexit when the first set is created; callers may run it earlier."""
     for s_enc, s_decs, handles in _STREAM_SETS.values():
         s_enc.synchronize()
         for s in s_decs:
@@ -95,6 +103,17 @@ def release_streams() -> None:
     _STREAM_SETS.clear()
 
 
+def _release_at_exit() -> None:
+    try:
+        if _STREAM_SETS and torch.cuda.is_initialized():
+            release_streams()
+    except Exception:   # interpreter shutdown: never turn a clean exit into a failure
+        pass
+
+
+atexit.register(_release_at_exit)
+
+
 class CaptionPipeline:
     def __init__(self, encoder: HipViTEncoder, prefix: HipPrefix, decoder: HipGPT2Decoder, cfg: GenConfig,
                  batch: int, prompt_ids: Sequence[int], device, depth: int = 2, gather=None,
@@ -102,7 +121,7 @@ class CaptionPipeline:
                  enc_group: int = 1):
         self.enc, self.pre, self.dec, self.cfg = encoder, prefix, decoder, cfg
         self.prompt_ids = list(prompt_ids)
-        self.device = torch.device(device)
+        self.device = torch.device("cuda", _device_index(device))
         if dec_lanes < 1 or dec_group < 1 or enc_group < 1:
             raise ValueError("dec_lanes, dec_group and enc_group must be >= 1")
         if dec_group % enc_group:

@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--max-new", type=int, default=24)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp8"],
                     help="fp8: MXFP8 ViT QKV/fc1/fc2 GEMMs (BASELINE configs[4]); the decoder stays bf16")
+    ap.add_argument("--dec-precision", default="auto", choices=["auto", "bf16", "fp32"],
+                    help="GPT-2 decoder arithmetic: auto = bf16 for --precision bf16 / fp8, fp32 for fp32; fp32 with "
+                         "--precision bf16 is the reference's own split (ViT under half-precision autocast, "
+                         "src/models/video_encoder.py:261-264; the decoder in fp32, text_decoder.py:131-144)")
     ap.add_argument("--mx-gemms", default="qkv,proj,fc1,fc2",
                     help="--precision fp8: the ViT block GEMMs run in MXFP8 (the others bf16)")
     ap.add_argument("--decode", default="hf_greedy", choices=["hf_greedy", "raw_greedy"])
@@ -551,7 +555,9 @@ def main():
     mx_gemms = tuple(g for g in args.mx_gemms.split(",") if g)
     enc = HipViTEncoder(sd, va, args.precision, dev, mx_gemms=mx_gemms)
     pre = HipPrefix(sd, ga.n_embd, device=dev)
-    dec = HipGPT2Decoder(sd, ga, "bf16" if args.precision == "fp8" else args.precision, dev)
+    if args.dec_precision == "auto":
+        args.dec_precision = "fp32" if args.precision == "fp32" else "bf16"
+    dec = HipGPT2Decoder(sd, ga, args.dec_precision, dev)
     if args.decode == "hf_greedy":
         cfg = GenConfig(args.max_new, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, not args.no_graph,
                         num_beams=args.beams)
@@ -690,14 +696,14 @@ def main():
     # with the near-tie evidence for every divergent caption (vcap/fidelity.py)
     parity = None
     dec_alone = None
-    if args.precision != "fp32" and args.parity:
+    if (args.precision != "fp32" or args.dec_precision != "fp32") and args.parity:
         parity = parity_report(sd, va, ga, video, pre, enc, dec, cfg, last, dev)
         torch.cuda.empty_cache()
     if args.decode_alone:
         with torch.cuda.stream(torch.cuda.Stream(dev)):
             _, pre_a = enc.encode(video, pre)
             step_s, prefill_s = decode_step_alone(dec, pre_a, cfg, ga)
-        wbytes = ga.weight_elems_per_step() * (4 if args.precision == "fp32" else 2)
+        wbytes = ga.weight_elems_per_step() * (4 if args.dec_precision == "fp32" else 2)
         dec_alone = {"what": (f"one token step of the B-row greedy decode graph" if args.beams == 1 else
                               f"one step of the device beam search graph ({B} x {args.beams} beams)") +
                              ", alone on the GPU (difference of a max_new-step and a 1-2-step graph)",
@@ -734,7 +740,7 @@ def main():
         att = launch_summary(probes["vit.attention"], M, attn_flops, attn_bytes)
         achieved = fc1["flops_per_launch"] / (fc1["avg_launch_ms"] / 1e3) / 1e12
         vit_exec = B * T * va.flops_per_frame(cls_tail=True)
-        dec_bytes = float(args.max_new * ga.weight_elems_per_step() * (4 if args.precision == "fp32" else 2))
+        dec_bytes = float(args.max_new * ga.weight_elems_per_step() * (4 if args.dec_precision == "fp32" else 2))
         t_roof = vit_exec / (peak * 1e12) + dec_bytes / (PEAK_HBM_GBS * 1e9)
         total = world * B * args.steps
         value = total / elapsed
@@ -742,7 +748,9 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "captions/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": {"bf16": "bf16", "fp8": f"mxfp8-e4m3 (ViT {'/'.join(enc.mx_gemms)}) + bf16"}.get(args.precision, "f32"),
+            "scaling": "weak", "vs_baseline": None, "dtype": ({"bf16": "bf16", "fp8": f"mxfp8-e4m3 (ViT {'/'.join(enc.mx_gemms)})"}.get(args.precision, "f32") +
+                       ("" if (args.precision == "fp32") == (args.dec_precision == "fp32") and args.precision != "fp8"
+                        else f" + {'f32' if args.dec_precision == 'fp32' else 'bf16'} decoder")),
             "data": "synthetic (seeded U[0,1) frames, ImageNet-normalised; seeded random-init weights)",
             "config": {"workload": f"batch={B} synthetic {T}x3x224x224 videos per GPU, {args.vit} + {args.gpt2}, "
                                    f"{args.decode if args.beams == 1 else f'beam-{args.beams}'} decode max_new {args.max_new} "
@@ -751,6 +759,7 @@ def main():
                        "vit": args.vit, "gpt2": args.gpt2, "batch_per_gpu": B, "global_batch": world * B,
                        "frames": T, "max_new_tokens": args.max_new,
                        "decode": args.decode if args.beams == 1 else f"beam-{args.beams} (device beam search, HF _beam_search)",
+                       "vit_precision": args.precision, "decoder_precision": args.dec_precision,
                        "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}",
                        "decode_block_cap": cfg.max_blocks,
                        "schedule": "serial" if args.serial else
@@ -780,7 +789,7 @@ def main():
             "roofline": {"bound": "mfma",
                          "kernel": {"bf16": "vit.fc1 vcap_gemm256_kernel<bf16,bf16,1>",
                                     "fp8": "vit.fc1 vcap_gemm256_kernel<mxfp8,mxfp8,4>"}.get(
-                                        args.precision, "vit.fc1 vcap_gemm_kernel<f32,f32,1>"),
+                                        args.precision, "vit.fc1 vcap_gemm256_kernel<f32,f32,1>"),
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": fc1_traffic(M, va.mlp, va.dim) if args.precision == "bf16" else None,
                          "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",

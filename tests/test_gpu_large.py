@@ -66,6 +66,20 @@ def test_medium_beam4_fp32_matches_reference(device, impl):
     assert np.array_equal(np.array(rows, dtype=np.int32), exp), (rows, exp)
 
 
+def test_medium_beam4_fp32_32_rows(device):
+    """The bench's configs[3] decode shape in fp32 (bench.py --dec-precision fp32: two batches of 4
+    videos x 4 beams = 32 decoder rows, whose f32 LayerNorm-prologue tiles take 16-row chunks): the
+    reference clips repeated to 8 sequences give the reference's beam-4 hypotheses for every copy."""
+    meta, g, va, ga, enc, pre, dec, video = _models(device)
+    prefix = torch.from_numpy(g["inputs_embeds"][:, :4].copy()).to(device)
+    reps = 8 // prefix.shape[0]
+    rows = search.beam_search_device(dec, prefix.repeat(reps, 1, 1).contiguous(), meta["prompt_ids"], num_beams=4,
+                                     max_new_tokens=40, min_new_tokens=8, no_repeat_ngram_size=3,
+                                     repetition_penalty=1.1, eos=ga.eos_token_id)
+    exp = g["beam4_ids"]
+    assert np.array_equal(np.array(rows, dtype=np.int32), np.concatenate([exp] * reps)), rows
+
+
 def test_l14_medium_bf16_close(device):
     """bf16 throughput mode at configs[3] shapes: encoder within 5e-2 abs of the fp32 reference
     (24 blocks of bf16 operand rounding), first greedy token identical where the reference's top-2

@@ -1169,7 +1169,10 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
   }
   const int ntb = rows_ntb(epi, a.N, a.max_blocks);
   if (nblk_out) *nblk_out = (a.N + ntb * 16 - 1) / (ntb * 16);
-  const bool one = a.M <= 16;
+  // f32 LayerNorm-prologue rows of > 512 features in 32-row chunks would need > 64 KiB of A tile
+  // beside the split-K buffers (GPT-2-medium fp32 beam search: 32 x 1024 x 4 B + 32 KiB > 160 KiB):
+  // such launches take 16-row chunks (two blockIdx.y chunks per 32 rows)
+  const bool one = a.M <= 16 || (pro == PRO_LN && dt != VCAP_DT_BF16 && a.K > 512);
 #define VCAP_ROWS(TT, PP, EE, NT) \
   return one ? launch_rows<TT, 1, NT, PP, EE>(a, s) : launch_rows<TT, 2, NT, PP, EE>(a, s);
 #define VCAP_ROWS_NT(TT, PP, EE)            \

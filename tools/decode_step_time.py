@@ -1,7 +1,7 @@
 """Per-token decode step cost (hipGraph, alone on the GPU) for the library named by VCAP_LIB
 (ablation builds).  Environment: B (sequences, default 8), GPT2 (arch, default gpt2), BEAMS
 (default 1 = HF-greedy graph; > 1 = the device beam search graph, preset "detailed" shape), CAP
-(decode grid cap)."""
+(decode grid cap), PREC (decoder arithmetic, bf16 or fp32)."""
 import os, sys, time
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
@@ -13,7 +13,7 @@ from vcap.model import GenConfig, HipGPT2Decoder
 name = os.environ.get("GPT2", "gpt2")
 ga = configs.gpt2_arch(name)
 dev = torch.device("cuda:0")
-dec = HipGPT2Decoder(weights.synthetic_gpt2(1, ga), ga, "bf16", dev)
+dec = HipGPT2Decoder(weights.synthetic_gpt2(1, ga), ga, os.environ.get("PREC", "bf16"), dev)
 from vcap import _native as N
 N.check(N.lib().vcap_set_gemm_policy(int(os.environ.get("VCAP_GEMM_POLICY", "0"))), "policy")
 s = torch.cuda.Stream()
@@ -40,5 +40,6 @@ with torch.cuda.stream(s):
             run()
         torch.cuda.synchronize()
         res[mx] = (time.perf_counter() - t) / 10 * 1e3
-print(f"{Path(os.environ.get('VCAP_LIB', 'base')).name} {name} B={B} beams={beams} cap={os.environ.get('CAP', '0')}: "
+print(f"{Path(os.environ.get('VCAP_LIB', 'base')).name} {name} {os.environ.get('PREC', 'bf16')} B={B} beams={beams} "
+      f"cap={os.environ.get('CAP', '0')}: "
       f"step {(res[hi]-res[lo])/(hi-lo)*1e3:.1f} us first {res[lo]*1e3:.0f} us")

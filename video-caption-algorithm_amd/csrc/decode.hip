@@ -76,10 +76,12 @@ VCAP_DEV const u32x4* packed_frag(const void* w, int tile, int nslab, int slab, 
 template <typename T, int MT, int NTB, int EPI>
 VCAP_DEV void rows_epilogue(const RowsGemmArgs& a, int m0, const float (*red)[MT * NTB * 256], const float* pre_bias,
                             const float* pre_res, float (*lg)[NTB * 16], const unsigned char (*s_rep)[NTB * 16],
-                            const unsigned char (*s_ban)[NTB * 16], int n0) {
+                            const unsigned char (*s_ban)[NTB * 16], int n0, int hsel = -1) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = a.M, N = a.N;
   const int row = tid >> 4, col = tid & 15;
+  // half-tile workgroup (hsel 0 / 1): only the 8 columns it computed are real
+  const bool mine = hsel < 0 || (col >> 3) == hsel;
 #pragma unroll
   for (int q = 0; q < MT * NTB; ++q) {
     const int e = tid + q * 256;
@@ -103,7 +105,7 @@ VCAP_DEV void rows_epilogue(const RowsGemmArgs& a, int m0, const float (*red)[MT
         }
       }
     } else if constexpr (EPI == EPI_RESID) {
-      if (ok) ((float*)a.out)[(long)m * a.ldo + n] = pre_res[q] + v;
+      if (ok && mine) ((float*)a.out)[(long)m * a.ldo + n] = pre_res[q] + v;
     } else if constexpr (EPI == EPI_GELU) {
       if (ok) ((T*)a.out)[(long)m * a.ldo + n] = Num<T>::from_f(gelu_tanh(v));
     } else if constexpr (EPI == EPI_STORE) {
@@ -307,7 +309,14 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   const int fr = lane & 15, fg = lane >> 4;
   const int M = a.M, N = a.N, K = a.K;
   const int m0 = blockIdx.y * MP;
-  const int n0 = blockIdx.x * NTB * 16;
+  // a.half (PRO_DIRECT residual GEMVs of NTB = 1): two workgroups per 16-column tile, each streaming
+  // the weights of 8 columns (lanes l and l ^ 8 load the same fragment: column (l & 7) of its half),
+  // so a K = 3072 projection spreads its weight stream over twice the CUs; the MFMAs, their order
+  // and every stored output are those of the full-tile workgroup
+  const bool half = EPI == EPI_RESID && NTB == 1 && a.half;
+  const int hsel = half ? (int)(blockIdx.x & 1) : -1;
+  const int n0 = half ? (int)(blockIdx.x >> 1) * 16 : blockIdx.x * NTB * 16;
+  const int wlane = half ? ((lane & 0x30) | (hsel << 3) | (lane & 7)) : lane;
   const int nslab = 4 * NSL;  // = K / KS
   const int g0 = wave * NSL;
   const int ntiles = (N + 15) >> 4;
@@ -348,7 +357,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   u32x4 wf[NSL][NTB];
 #pragma unroll
   for (int j = 0; j < NTB; ++j) {
-    const u32x4* wp = packed_frag(a.w, min(n0 / 16 + j, ntiles - 1), nslab, g0, lane);
+    const u32x4* wp = packed_frag(a.w, min(n0 / 16 + j, ntiles - 1), nslab, g0, wlane);
 #pragma unroll
     for (int s = 0; s < NSL; ++s) wf[s][j] = vcap_dec_wload<MT == 1>(a.w, wp + s * 64);
   }
@@ -460,7 +469,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
       for (int r = 0; r < 4; ++r) red[wave][(i * NTB + j) * 256 + (fg * 4 + r) * 16 + fr] = acc[i][j][r];
   if constexpr (EPI == EPI_LOGITS) toks.template mark<NTB>(a, m0, n0, s_rep, s_ban);
   __syncthreads();
-  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0);
+  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0, hsel);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -901,7 +910,8 @@ static int allow_lds(Kern k, int& limit) {
 
 template <typename T, int MT, int NTB, int PRO, int EPI, int NSL>
 static hipError_t launch_gemv(const RowsGemmArgs& a, hipStream_t s) {
-  const dim3 grid((a.N + NTB * 16 - 1) / (NTB * 16), (a.M + MT * 16 - 1) / (MT * 16));
+  const int half = EPI == EPI_RESID && NTB == 1 && a.half ? 2 : 1;
+  const dim3 grid(half * ((a.N + NTB * 16 - 1) / (NTB * 16)), (a.M + MT * 16 - 1) / (MT * 16));
   const size_t lds = PRO == PRO_LN ? (size_t)MT * 16 * a.K * sizeof(T) : 0;
   static int limit = 0;
   if ((size_t)allow_lds(vcap_rows_gemv_kernel<T, MT, NTB, PRO, EPI, NSL>, limit) < lds) return hipErrorInvalidValue;
@@ -1169,12 +1179,19 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
   }
   const int ntb = rows_ntb(epi, a.N, a.max_blocks);
   if (nblk_out) *nblk_out = (a.N + ntb * 16 - 1) / (ntb * 16);
+  // residual projections (attn / mlp c_proj: N = E, 48 tiles for GPT-2) on whole tiles use a
+  // workgroup per 8 columns instead of 16 when the grid may double: the per-CU weight stream, not
+  // the MFMAs, bounds these GEMVs (K = 3072: 98 KB of weights per workgroup)
+  RowsGemmArgs ah = a;
+  const int tiles = (a.N + 15) / 16;
+  ah.half = pro == PRO_DIRECT && epi == EPI_RESID && ntb == 1 && a.M <= 32 &&
+            (a.max_blocks <= 0 ? 2 * tiles <= vcap_device_cus() : 2 * tiles <= a.max_blocks);
   // f32 LayerNorm-prologue rows of > 512 features in 32-row chunks would need > 64 KiB of A tile
   // beside the split-K buffers (GPT-2-medium fp32 beam search: 32 x 1024 x 4 B + 32 KiB > 160 KiB):
   // such launches take 16-row chunks (two blockIdx.y chunks per 32 rows)
   const bool one = a.M <= 16 || (pro == PRO_LN && dt != VCAP_DT_BF16 && a.K > 512);
 #define VCAP_ROWS(TT, PP, EE, NT) \
-  return one ? launch_rows<TT, 1, NT, PP, EE>(a, s) : launch_rows<TT, 2, NT, PP, EE>(a, s);
+  return one ? launch_rows<TT, 1, NT, PP, EE>(ah, s) : launch_rows<TT, 2, NT, PP, EE>(ah, s);
 #define VCAP_ROWS_NT(TT, PP, EE)            \
   if (ntb == 4) { VCAP_ROWS(TT, PP, EE, 4) } \
   if (ntb == 2) { VCAP_ROWS(TT, PP, EE, 2) } \

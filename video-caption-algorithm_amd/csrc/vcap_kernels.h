@@ -62,6 +62,7 @@ struct RowsGemmArgs {
   int min_new, eos;
   int max_blocks;  // 0: one 16-column tile per workgroup; > 0: widen tiles to stay near this grid
   float* proc_out;  // EPI_LOGITS, optional [M, N]: the processed scores (sampling mode)
+  int half;         // set by vcap_rows_gemm_dispatch: residual GEMV tiles split into two 8-column workgroups
 };
 
 // ---- sampling warpers + draw (csrc/sample.hip)

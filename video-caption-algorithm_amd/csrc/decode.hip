@@ -473,6 +473,51 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Residual GEMV (PRO_DIRECT + EPI_RESID, <= 16 rows, one 16-column tile per workgroup) whose K range
+// needs more fragments than 4 waves hold: the f32 mlp c_proj (K = 3072: 48 slabs of 16 per wave
+// would be 96 16-byte fragments per lane).  8 waves (two per SIMD) of NSL slabs each, every load
+// issued up front as in vcap_rows_gemv_kernel, split-K partials summed through LDS in a fixed order
+// ((w0 + w1) + (w2 + w3)) + ((w4 + w5) + (w6 + w7)).
+template <typename T, int NSL>
+__global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
+  constexpr int E = Frag<T>::kElems, KS = 4 * E;
+  __shared__ __attribute__((aligned(16))) float red[8][256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int M = a.M, N = a.N;
+  const int n0 = blockIdx.x * 16;
+  const int nslab = 8 * NSL, g0 = wave * NSL;
+  const int ntiles = (N + 15) >> 4;
+  u32x4 af[NSL];
+  const long xo = (long)min(fr, M - 1) * a.ldx + fg * E;
+#pragma unroll
+  for (int s = 0; s < NSL; ++s) af[s] = vcap_dec_aload(a.x, (xo + (g0 + s) * KS) * (long)sizeof(T));
+  asm volatile("" ::: "memory");  // the activation loads issue before the weights
+  u32x4 wf[NSL];
+  const u32x4* wp = packed_frag(a.w, min((int)blockIdx.x, ntiles - 1), nslab, g0, lane);
+#pragma unroll
+  for (int s = 0; s < NSL; ++s) wf[s] = vcap_dec_wload<true>(a.w, wp + s * 64);
+  const int row = (tid >> 4) & 15, col = tid & 15;
+  const int mc = min(row, M - 1), nc = min(n0 + col, N - 1);
+  const float bl = *(a.bias ? a.bias + nc : (const float*)a.x);
+  const float pre_bias = a.bias ? bl : 0.f;
+  const float pre_res = ((const float*)a.out)[(long)mc * a.ldo + nc];
+  asm volatile("" : "+v"(af[0])::"memory");
+  f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NSL; ++s) acc = mfma_frag(af[s], wf[s], acc, (T*)nullptr);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][(fg * 4 + r) * 16 + fr] = acc[r];
+  __syncthreads();
+  if (tid < 256 && row < M && n0 + col < N) {
+    const int e = tid;
+    const float v = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) +
+                    ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e])) + pre_bias;
+    ((float*)a.out)[(long)row * a.ldo + n0 + col] = pre_res + v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // General rows kernel (prefill rows, f32 parity mode, shapes outside the GEMV instantiations):
 // rows [m0, m0 + MT*16) of a blockIdx.y row chunk; weights streamed in double-buffered chunks of
 // U slabs; PRO_DIRECT A fragments ride along with each weight chunk in registers, PRO_LN rows
@@ -953,6 +998,12 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
       try_gemv<T, MT, NTB, PRO, EPI, 12>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 16>(nsl, a, s, err) ||
       try_gemv<T, MT, NTB, PRO, EPI, 24>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 32>(nsl, a, s, err))
     return err;
+  if constexpr (sizeof(T) == 4 && MT == 1 && NTB == 1 && PRO == PRO_DIRECT && EPI == EPI_RESID) {
+    if (nsl == 48) {  // f32 mlp c_proj of GPT-2 small (K = 3072): 8 waves x 24 slabs
+      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 24>), dim3((a.N + 15) / 16), dim3(512), 0, s, a);
+      return hipGetLastError();
+    }
+  }
   return launch_generic<T, MT, NTB, PRO, EPI>(a, s);
 }
 

@@ -730,10 +730,19 @@ def main():
         def fc1_flops(rows):
             return 2.0 * rows * va.mlp * va.dim
 
+        # bf16 ViT-B/16 frames (192 < tokens <= 208): the QKV projection and the attention run as one
+        # kernel (vcap_vit_qkv_attention) and the "vit.attention" probe times it; otherwise the probe
+        # times the attention kernel alone
+        fused_attn = (args.precision in ("bf16", "fp8") and 192 < va.tokens <= 208
+                      and not {"qkv", "proj"} & set(enc.mx_gemms))
+
         def attn_flops(rows):
-            return 4.0 * (rows // va.tokens) * va.heads * va.tokens * va.tokens * 64
+            core = 4.0 * (rows // va.tokens) * va.heads * va.tokens * va.tokens * 64
+            return core + (2.0 * rows * 3 * va.dim * va.dim if fused_attn else 0.0)
 
         def attn_bytes(rows):
+            if fused_attn:   # LayerNorm rows in, attention rows out (q / k / v stay on chip), weights
+                return float(2 * rows * va.dim * ab + 3 * va.dim * va.dim * ab)
             return float(rows * 3 * va.dim * ab + rows * va.dim * (1 if args.precision == "fp8" else ab))
 
         fc1 = launch_summary(probes["vit.fc1"], M, fc1_flops)
@@ -798,7 +807,9 @@ def main():
                          "timing": "HIP events around each fc1 launch on its stream inside the timed region "
                                    "(vcap_probe_*), read right after it; priced per launch population",
                          "other_populations": fc1["other_populations"]},
-            "attention": {"kernel": "vit.attention", "bound": "hbm", "avg_launch_ms": att["avg_launch_ms"],
+            "attention": {"kernel": ("vit.attention = vcap_vit_qkv_attention_kernel (QKV projection + attention)"
+                                     if fused_attn else "vit.attention"),
+                          "bound": "mfma" if fused_attn else "hbm", "avg_launch_ms": att["avg_launch_ms"],
                           "launch_rows": M, "launches": att["launches"],
                           "achieved_tflops": att["flops_per_launch"] / (att["avg_launch_ms"] / 1e3) / 1e12,
                           "frac_of_mfma_peak": att["flops_per_launch"] / (att["avg_launch_ms"] / 1e3) / 1e12 / peak,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 11
+#define VCAP_ABI_VERSION 12
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -146,6 +146,14 @@ int vcap_gemm(int in_dtype, int out_dtype, const void* A, int64_t lda, const voi
 int vcap_layernorm(int out_dtype, const float* x, int64_t ldx, void* y, int64_t ldy, const float* gamma,
                    const float* beta, int rows, int dim, float eps, void* stream);
 int vcap_vit_attention(int dtype, const void* qkv, void* out, int frames, int tokens, int heads, void* stream);
+/* Fused QKV projection + attention (bf16; 192 < tokens <= 208, i.e. ViT-B/16 frames): xn
+ * [frames*tokens, heads*64] bf16 (the LayerNorm output), wqkv [3*heads*64, heads*64] bf16, bqkv
+ * [3*heads*64] f32 -> out [frames*tokens, heads*64] bf16 (cls_only: [frames, heads*64], the class
+ * token's row).  Bit-identical to vcap_gemm (bias, bf16 out) into a qkv buffer followed by
+ * vcap_vit_attention; q / k / v stay on chip.  Replaces timm Attention.qkv + the attention core
+ * (src/models/video_encoder.py:112-121).  VCAP_E_UNSUPPORTED outside that shape. */
+int vcap_vit_qkv_attention(const void* xn, const void* wqkv, const float* bqkv, void* out, int frames, int tokens,
+                           int heads, int cls_only, void* stream);
 
 /* ---- frame preprocessing (core/preprocessing/frame_loader.py:34-45: torchvision Resize((S, S)) on
  *      PIL images -> ToTensor -> Normalize): decoded RGB frames uint8 [n, in_h, in_w, 3] (device)

@@ -733,6 +733,18 @@ int vcap_vit_attention(int dtype, const void* qkv, void* out, int frames, int to
   return 0;
 }
 
+int vcap_vit_qkv_attention(const void* xn, const void* wqkv, const float* bqkv, void* out, int frames, int tokens,
+                           int heads, int cls_only, void* stream) {
+  if (!xn || !wqkv || !bqkv || !out || frames <= 0 || tokens <= 0 || heads <= 0)
+    return fail(VCAP_E_ARG, "vcap_vit_qkv_attention: bad arguments");
+  if (!vcap_vit_qkv_attention_supported(VCAP_DT_BF16, tokens, heads))
+    return fail(VCAP_E_UNSUPPORTED, "vcap_vit_qkv_attention: needs 192 < tokens <= 208 and heads*64 <= 4096");
+  VCAP_TRY(vcap_vit_qkv_attention_dispatch(xn, wqkv, bqkv, out, frames, tokens, heads, cls_only ? 1 : 0,
+                                           (hipStream_t)stream),
+           "vcap_vit_qkv_attention");
+  return 0;
+}
+
 int vcap_vit_attention_mx(const void* qkv, void* out, uint8_t* out_scales, int frames, int tokens, int heads,
                           void* stream) {
   if (!qkv || !out || !out_scales || frames <= 0 || tokens <= 0 || heads <= 0)
@@ -812,6 +824,15 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
     else
       VCAP_TRY(vcap_layernorm_dispatch(adt, w.x, D, w.xn, D, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s), "norm1");
     GemmEpi e1{ly.qkv_b, nullptr, 0, 0, 0, 0, 0, 0, 0, mq ? w.xn_s : nullptr, mq ? ly.qkv_ws : nullptr, nullptr};
+#ifndef VCAP_AB_NOFUSE
+    if (!mq && !mp && vcap_vit_qkv_attention_supported(adt, N, d->heads)) {
+      // QKV projection + attention in one kernel: q / k / v stay on chip
+      ProbeScope ps(probe_attn, s, M);
+      VCAP_TRY(vcap_vit_qkv_attention_dispatch(w.xn, ly.qkv_w, ly.qkv_b, w.attn, BT, N, d->heads, last, s),
+               "qkv_attention");
+    } else
+#endif
+    {
     {
       ProbeScope ps("vit.qkv", s, M);
       VCAP_TRY(vcap_gemm_dispatch(dq, adt, w.xn, D, ly.qkv_w, D, w.qkv, 3 * D, M, 3 * D, D, e1, s), "qkv");
@@ -822,6 +843,7 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
         VCAP_TRY(vcap_vit_attention_mx_dispatch(w.qkv, w.attn, w.xn_s, BT, N, d->heads, s, last), "attention");
       else
         VCAP_TRY(vcap_vit_attention_dispatch(adt, w.qkv, w.attn, BT, N, d->heads, s, last), "attention");
+    }
     }
     // MXFP8: the attention output arrives as MXFP8 (its scales reuse xn_s, free until norm2)
     GemmEpi e2{ly.proj_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, mp ? w.xn_s : nullptr,

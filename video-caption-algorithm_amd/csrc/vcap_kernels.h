@@ -106,6 +106,11 @@ hipError_t vcap_layernorm_dispatch(int out_dt, const float* x, long ldx, void* y
 // cls_only: only the class-token query of each (frame, head), written to compact row `frame`
 hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s,
                                        int cls_only = 0);
+// fused QKV projection + attention (bf16, 192 < N <= 208): xn [BT*N, H*64] LayerNorm output, wqkv
+// [3*H*64, H*64], bqkv [3*H*64] -> out as vcap_vit_attention_dispatch's
+bool vcap_vit_qkv_attention_supported(int dt, int N, int H);
+hipError_t vcap_vit_qkv_attention_dispatch(const void* xn, const void* wqkv, const float* bqkv, void* out, int BT,
+                                           int N, int H, int cls_only, hipStream_t s);
 hipError_t vcap_vit_attention_mx_dispatch(const void* qkv, void* out, uint8_t* oscale, int BT, int N, int H,
                                           hipStream_t s, int cls_only = 0);
 hipError_t vcap_patchify_dispatch(int dt, const float* frames, void* patches, float* x, const float* cls,

@@ -449,6 +449,199 @@ static hipError_t launch_attn(const void* qkv, void* out, int BT, int N, int H, 
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fused QKV projection + attention (bf16, ViT-B/16 frame: 197 tokens, head_dim 64).  One workgroup
+// (8 waves) per (frame, head): it computes the head's 192 q / k / v features of the frame's 208
+// (padded) tokens from the LayerNorm output and the head's 192 weight rows, writes them as bf16
+// straight into the attention's LDS images and runs the attention above on them - q / k / v never
+// leave the CU (the unfused pair writes 3 x 768 bf16 per token to HBM and reads them back).
+//  * GEMM: C^T[feature][token] with the weight fragment as the MFMA A operand (each lane ends up
+//    with 4 consecutive features of one token = 8 contiguous bytes of a [token][64] image) and the
+//    K order of vcap_gemm256_kernel (32-wide sub-steps, lane group g = K [8g, 8g + 8)), so every
+//    q / k / v value, its bias add and its bf16 rounding are those of the unfused QKV GEMM and the
+//    output is bit-identical to QKV GEMM + vcap_vit_attention_bf16_kernel;
+//  * waves 4 (feature groups of 3 tiles) x 2 (token groups of 7 / 6 tiles): 21 / 18 16x16
+//    accumulators per wave;
+//  * K-tiles of 64 (208 token rows + 192 weight rows x 128 B = 50 KiB) stream by LDS-DMA through a
+//    3-deep ring (150 KiB: one workgroup per CU), rows XOR-swizzled on the source like the
+//    GEMM's; token rows past N re-read row N - 1 (what the unfused attention stages);
+//  * the ring's first 78 KiB then hold the K, V and Q images ([token][64], chunk ^ (token & 7)).
+// Grid: frames x heads, XCD-aware when frames % 8 == 0 (workgroup b runs on XCD b % 8; the heads
+// of one frame go to the same XCD back to back so its LayerNorm rows are re-read from that L2).
+namespace qa {
+constexpr int TT = 13, FT = 12;                // token tiles (208 tokens), feature tiles (q, k, v)
+constexpr int RT = TT * 16, RW = FT * 16;      // 208 token rows, 192 weight rows per K-tile
+constexpr int STAGE = (RT + RW) * 128;         // 51200 B
+constexpr int NSTAGE = 3;
+constexpr int LDS = NSTAGE * STAGE;            // 153600 B
+constexpr int BLKS = (RT + RW) / 8;            // 50 LDS-DMA wave instructions (8 rows) per K-tile
+constexpr int NB_MAX = (BLKS + 7) / 8;         // 7 (waves 0, 1), 6 (waves 2..7)
+}  // namespace qa
+
+template <bool TWO_NB>
+VCAP_DEV void qa_wait_older(bool older) {
+  // all but this wave's most recent K-tile of LDS-DMA landed
+  if (older) {
+    if constexpr (TWO_NB) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+__global__ __launch_bounds__(512) void vcap_vit_qkv_attention_kernel(const bf16_t* __restrict__ xn,
+                                                                     const bf16_t* __restrict__ wqkv,
+                                                                     const float* __restrict__ bqkv,
+                                                                     bf16_t* __restrict__ out, int BT, int N, int H,
+                                                                     int cls_only) {
+  using namespace qa;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int D = H * 64;  // = K of the projection
+  const int b = blockIdx.x;
+  int bt, h;
+  if ((BT & 7) == 0) {
+    const int x = b & 7, j = b >> 3;
+    bt = (j / H) * 8 + x;
+    h = j - (j / H) * H;
+  } else {
+    bt = b / H;
+    h = b - bt * H;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int fgrp = wave & 3, tgrp = wave >> 2;
+  const int t0 = tgrp * 7, ntt = tgrp ? TT - 7 : 7;
+
+  // this thread's LDS-DMA sources (K-tile 0): block blk = wave + 8 i stages rows blk*8 .. +8
+  const char* src[NB_MAX];
+#pragma unroll
+  for (int i = 0; i < NB_MAX; ++i) {
+    const int blk = min(wave + 8 * i, BLKS - 1);
+    const int lr = blk * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (lr & 7);
+    const bf16_t* p;
+    if (lr < RT) {
+      p = xn + ((long)bt * N + min(lr, N - 1)) * D;
+    } else {
+      const int f = lr - RT;  // 0..191: q / k / v feature f & 63 of head h
+      p = wqkv + ((long)(f >> 6) * D + h * 64 + (f & 63)) * D;
+    }
+    src[i] = (const char*)(p + c * 8);
+  }
+  const int nb = wave < BLKS - 8 * (NB_MAX - 1) ? NB_MAX : NB_MAX - 1;  // 7 for waves 0, 1
+  auto stage = [&](int kt) {
+    char* dst = smem + (kt % NSTAGE) * STAGE;
+#pragma unroll
+    for (int i = 0; i < NB_MAX; ++i)
+      if (i < nb) glds16_attn(src[i] + kt * 128, dst + (wave + 8 * i) * 1024);
+  };
+
+  f32x4 acc[3][7];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = D / 64;
+  stage(0);
+  if (nk > 1) stage(1);
+  u32x4 wfs[2][3], tfs[2][7];
+  for (int kt = 0; kt < nk; ++kt) {
+    if (nb == NB_MAX) qa_wait_older<true>(kt + 1 < nk);
+    else qa_wait_older<false>(kt + 1 < nk);
+    __syncthreads();  // K-tile kt landed for every wave; ring slot (kt + 2) % 3 read by all
+    if (kt + 2 < nk) stage(kt + 2);
+    const char* Tb = smem + (kt % NSTAGE) * STAGE;
+    const char* Wb = Tb + RT * 128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u32x4 (&wf)[3] = wfs[s];
+      u32x4 (&tf)[7] = tfs[s];
+      {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int row = (fgrp * 3 + i) * 16 + fr;
+        wf[i] = *reinterpret_cast<const u32x4*>(Wb + row * 128 + (((s * 4 + fg) ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        if (j < ntt) {
+          const int row = (t0 + j) * 16 + fr;
+          tf[j] = *reinterpret_cast<const u32x4*>(Tb + row * 128 + (((s * 4 + fg) ^ (row & 7)) << 4));
+        }
+      }
+      }
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+          if (j < ntt) acc[i][j] = mfma_frag(wf[i], tf[j], acc[i][j], (bf16_t*)nullptr);
+    }
+  }
+  __syncthreads();  // every wave's fragment reads done: the ring becomes the K / V / Q images
+
+  char* Ks = smem;
+  char* Vs = smem + RT * 128;
+  char* Qs = smem + 2 * RT * 128;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int ft = fgrp * 3 + i, part = ft >> 2;        // 0 q, 1 k, 2 v
+    const int d0 = (ft & 3) * 16 + 4 * fg;              // this lane's 4 features of the head
+    const f32x4 bias = *reinterpret_cast<const f32x4*>(bqkv + part * D + h * 64 + d0);
+    char* img = part == 0 ? Qs : (part == 1 ? Ks : Vs);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      if (j < ntt) {
+        const int tok = (t0 + j) * 16 + fr;
+        const f32x4 v = acc[i][j] + bias;
+        const u32x2 p = (u32x2){pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
+        *reinterpret_cast<u32x2*>(img + tok * 128 + (((d0 >> 3) ^ (tok & 7)) << 4) + (d0 & 7) * 2) = p;
+      }
+    }
+  }
+  __syncthreads();
+
+  constexpr int WAVES = 8, QT_MAX = 2;
+  const int qtiles = cls_only ? 1 : (N + 15) / 16;
+#pragma unroll
+  for (int i = 0; i < QT_MAX; ++i) {
+    const int qt = wave + i * WAVES;
+    if (qt >= qtiles) break;
+    u32x4 qf[2];
+    const int qrow = qt * 16 + fr;  // rows past N hold row N - 1's q (clamped staging)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      qf[s] = *reinterpret_cast<const u32x4*>(Qs + qrow * 128 + (((s * 4 + fg) ^ (qrow & 7)) << 4));
+    f32x4 o[4];
+    float inv;
+    attn_bf16_qtile<14, 13>(Ks, Vs, qf, N, o, inv);
+    const int q = qt * 16 + fr;
+    const bool keep = q < N && (!cls_only || q == 0);
+    const long row = cls_only ? (long)bt : (long)bt * N + q;
+    attn_commit<false>(attn_pack<false>(o, inv, row, keep), out, D, h, nullptr, 0);
+  }
+}
+
+bool vcap_vit_qkv_attention_supported(int dt, int N, int H) {
+  return dt == VCAP_DT_BF16 && N > 12 * 16 && N <= 13 * 16 && H > 0 && H * 64 <= 4096;
+}
+
+hipError_t vcap_vit_qkv_attention_dispatch(const void* xn, const void* wqkv, const float* bqkv, void* out, int BT,
+                                           int N, int H, int cls_only, hipStream_t s) {
+  if (!vcap_vit_qkv_attention_supported(VCAP_DT_BF16, N, H) || BT <= 0 || !bqkv) return hipErrorInvalidValue;
+  static bool configured = false;
+  if (!configured) {
+    hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_qkv_attention_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, qa::LDS);
+    if (e != hipSuccess) return e;
+    configured = true;
+  }
+  hipLaunchKernelGGL(vcap_vit_qkv_attention_kernel, dim3(BT * H), dim3(512), qa::LDS, s, (const bf16_t*)xn,
+                     (const bf16_t*)wqkv, bqkv, (bf16_t*)out, BT, N, H, cls_only);
+  return hipGetLastError();
+}
+
 // bf16 kernel choice by padded key count; KE = key tiles that can hold real keys
 template <bool MXO>
 static hipError_t attn_bf16_dispatch(const void* qkv, void* out, uint8_t* oscale, int BT, int N, int H,

@@ -16,7 +16,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
 DT_F32, DT_BF16, DT_MXFP8 = 0, 1, 2
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
@@ -89,6 +89,7 @@ SIGNATURES = {
                         i32, vp]),
     "vcap_layernorm": (i32, [i32, vp, i64, vp, i64, vp, vp, i32, i32, f32, vp]),
     "vcap_vit_attention": (i32, [i32, vp, vp, i32, i32, i32, vp]),
+    "vcap_vit_qkv_attention": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, vp]),
     "vcap_frames_workspace_bytes": (sz, [i32, i32, i32, i32, i32]),
     "vcap_frames_preprocess": (i32, [vp, i32, i32, i32, i32, i32, fp, fp, vp, vp, vp, sz, vp]),
     "vcap_jpeg_probe": (i32, [vp, sz, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),

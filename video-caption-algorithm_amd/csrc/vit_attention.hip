@@ -478,6 +478,16 @@ constexpr int BLKS = (RT + RW) / 8;            // 50 LDS-DMA wave instructions (
 constexpr int NB_MAX = (BLKS + 7) / 8;         // 7 (waves 0, 1), 6 (waves 2..7)
 }  // namespace qa
 
+// A bare workgroup barrier.  __syncthreads() would also make every wave drain ALL its vector memory
+// operations first (s_waitcnt vmcnt(0)), i.e. wait for the K-tile DMA issued one iteration ago and
+// cut the ring's look-ahead to one K-tile; the waits this kernel needs are explicit (qa_wait_older
+// before, lgkmcnt(0) after the image writes).
+VCAP_DEV void qa_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <bool TWO_NB>
 VCAP_DEV void qa_wait_older(bool older) {
   // all but this wave's most recent K-tile of LDS-DMA landed
@@ -513,11 +523,18 @@ __global__ __launch_bounds__(512) void vcap_vit_qkv_attention_kernel(const bf16_
   const int fgrp = wave & 3, tgrp = wave >> 2;
   const int t0 = tgrp * 7, ntt = tgrp ? TT - 7 : 7;
 
-  // this thread's LDS-DMA sources (K-tile 0): block blk = wave + 8 i stages rows blk*8 .. +8
+  // The two wave groups (tgrp 0 = waves 0-3, one per SIMD, token tiles 0-6; tgrp 1 = waves 4-7,
+  // tiles 7-12) run one barrier apart: while one group issues its 42 MFMAs of a K-tile the other
+  // reads its fragments of the K-tile and issues its half of the LDS-DMA of the K-tile two ahead,
+  // so every SIMD always has one wave with MFMAs to issue (vcap_gemm256_kernel's stagger).
+  // Group g stages LDS-DMA blocks 25 g .. 25 g + 24 of each K-tile (8 rows = 1 KiB each; token rows
+  // 0-207 are blocks 0-25, weight rows blocks 26-49): wave wig of the group blocks wig + 4 i.
+  const int wig = wave & 3;
+  const int npg = wig == 0 ? NB_MAX : NB_MAX - 1;  // 7 / 6 / 6 / 6 = 25 pieces per group
   const char* src[NB_MAX];
 #pragma unroll
   for (int i = 0; i < NB_MAX; ++i) {
-    const int blk = min(wave + 8 * i, BLKS - 1);
+    const int blk = min(25 * tgrp + wig + 4 * i, BLKS - 1);
     const int lr = blk * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (lr & 7);
     const bf16_t* p;
@@ -529,12 +546,15 @@ __global__ __launch_bounds__(512) void vcap_vit_qkv_attention_kernel(const bf16_
     }
     src[i] = (const char*)(p + c * 8);
   }
-  const int nb = wave < BLKS - 8 * (NB_MAX - 1) ? NB_MAX : NB_MAX - 1;  // 7 for waves 0, 1
-  auto stage = [&](int kt) {
+  auto stage = [&](int kt) {  // this wave's pieces of K-tile kt
     char* dst = smem + (kt % NSTAGE) * STAGE;
 #pragma unroll
     for (int i = 0; i < NB_MAX; ++i)
-      if (i < nb) glds16_attn(src[i] + kt * 128, dst + (wave + 8 * i) * 1024);
+      if (i < npg) glds16_attn(src[i] + kt * 128, dst + (25 * tgrp + wig + 4 * i) * 1024);
+  };
+  auto wait_tile = [&](bool older) {  // this wave's pieces of all but its latest staged K-tile
+    if (npg == NB_MAX) qa_wait_older<true>(older);
+    else qa_wait_older<false>(older);
   };
 
   f32x4 acc[3][7];
@@ -546,40 +566,48 @@ __global__ __launch_bounds__(512) void vcap_vit_qkv_attention_kernel(const bf16_
   const int nk = D / 64;
   stage(0);
   if (nk > 1) stage(1);
-  u32x4 wfs[2][3], tfs[2][7];
+  wait_tile(nk > 1);
+  qa_barrier();                      // K-tile 0 landed
+  if (tgrp == 1) qa_barrier();       // group 1 runs one barrier behind
   for (int kt = 0; kt < nk; ++kt) {
-    if (nb == NB_MAX) qa_wait_older<true>(kt + 1 < nk);
-    else qa_wait_older<false>(kt + 1 < nk);
-    __syncthreads();  // K-tile kt landed for every wave; ring slot (kt + 2) % 3 read by all
-    if (kt + 2 < nk) stage(kt + 2);
+    // ---- read phase: fragments of K-tile kt, this wave's pieces of K-tile kt + 2 (into the slot
+    // of K-tile kt - 1, whose reads both groups finished before the last barrier)
     const char* Tb = smem + (kt % NSTAGE) * STAGE;
     const char* Wb = Tb + RT * 128;
+    u32x4 wf[2][3], tf[2][7];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      u32x4 (&wf)[3] = wfs[s];
-      u32x4 (&tf)[7] = tfs[s];
-      {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const int row = (fgrp * 3 + i) * 16 + fr;
-        wf[i] = *reinterpret_cast<const u32x4*>(Wb + row * 128 + (((s * 4 + fg) ^ (row & 7)) << 4));
+        wf[s][i] = *reinterpret_cast<const u32x4*>(Wb + row * 128 + (((s * 4 + fg) ^ (row & 7)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < 7; ++j) {
         if (j < ntt) {
           const int row = (t0 + j) * 16 + fr;
-          tf[j] = *reinterpret_cast<const u32x4*>(Tb + row * 128 + (((s * 4 + fg) ^ (row & 7)) << 4));
+          tf[s][j] = *reinterpret_cast<const u32x4*>(Tb + row * 128 + (((s * 4 + fg) ^ (row & 7)) << 4));
         }
       }
-      }
+    }
+    if (kt + 2 < nk) stage(kt + 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragments in registers before the barrier
+    wait_tile(kt + 2 < nk);                             // this wave's pieces of K-tile kt + 1 landed
+    qa_barrier();
+    // ---- MFMA phase
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 7; ++j)
 #pragma unroll
         for (int i = 0; i < 3; ++i)
-          if (j < ntt) acc[i][j] = mfma_frag(wf[i], tf[j], acc[i][j], (bf16_t*)nullptr);
-    }
+          if (j < ntt) acc[i][j] = mfma_frag(wf[s][i], tf[s][j], acc[i][j], (bf16_t*)nullptr);
+    __builtin_amdgcn_s_setprio(0);
+    qa_barrier();
   }
-  __syncthreads();  // every wave's fragment reads done: the ring becomes the K / V / Q images
+  if (tgrp == 0) qa_barrier();       // balance group 1's extra barrier
+  qa_barrier();                      // every wave's fragment reads done: the ring becomes the images
 
   char* Ks = smem;
   char* Vs = smem + RT * 128;
@@ -600,7 +628,8 @@ __global__ __launch_bounds__(512) void vcap_vit_qkv_attention_kernel(const bf16_
       }
     }
   }
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the images written before any wave reads them
+  qa_barrier();
 
   constexpr int WAVES = 8, QT_MAX = 2;
   const int qtiles = cls_only ? 1 : (N + 15) / 16;

@@ -45,7 +45,8 @@ for name, c in acc.items():
     kernels[short] = k
     if any(t in short for t in ("rows_gemv", "decode_attention", "decode_finalize")) and fetch is not None:
         dec_bytes += (sum(c["FETCH_SIZE"]) * 2 + sum(c.get("WRITE_SIZE", [0]))) * 1000
-vit = {k: v for k, v in kernels.items() if "gemm256" in k or "vit_attention" in k or "layernorm" in k}
+vit = {k: v for k, v in kernels.items()
+       if "gemm256" in k or "vit_attention" in k or "qkv_attention" in k or "layernorm" in k}
 res = {"source": "rocprofv3 --pmc passes (tools/pmc.sh) of python bench.py --serial --steps 2 --warmup 1",
        "vit_rows": vit_rows,
        "vit_kernels": vit,

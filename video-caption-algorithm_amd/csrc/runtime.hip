@@ -824,26 +824,21 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
     else
       VCAP_TRY(vcap_layernorm_dispatch(adt, w.x, D, w.xn, D, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s), "norm1");
     GemmEpi e1{ly.qkv_b, nullptr, 0, 0, 0, 0, 0, 0, 0, mq ? w.xn_s : nullptr, mq ? ly.qkv_ws : nullptr, nullptr};
-#ifndef VCAP_AB_NOFUSE
     if (!mq && !mp && vcap_vit_qkv_attention_supported(adt, N, d->heads)) {
       // QKV projection + attention in one kernel: q / k / v stay on chip
       ProbeScope ps(probe_attn, s, M);
       VCAP_TRY(vcap_vit_qkv_attention_dispatch(w.xn, ly.qkv_w, ly.qkv_b, w.attn, BT, N, d->heads, last, s),
                "qkv_attention");
-    } else
-#endif
-    {
-    {
-      ProbeScope ps("vit.qkv", s, M);
-      VCAP_TRY(vcap_gemm_dispatch(dq, adt, w.xn, D, ly.qkv_w, D, w.qkv, 3 * D, M, 3 * D, D, e1, s), "qkv");
-    }
-    {
+    } else {
+      {
+        ProbeScope ps("vit.qkv", s, M);
+        VCAP_TRY(vcap_gemm_dispatch(dq, adt, w.xn, D, ly.qkv_w, D, w.qkv, 3 * D, M, 3 * D, D, e1, s), "qkv");
+      }
       ProbeScope ps(probe_attn, s, M);
       if (mp)
         VCAP_TRY(vcap_vit_attention_mx_dispatch(w.qkv, w.attn, w.xn_s, BT, N, d->heads, s, last), "attention");
       else
         VCAP_TRY(vcap_vit_attention_dispatch(adt, w.qkv, w.attn, BT, N, d->heads, s, last), "attention");
-    }
     }
     // MXFP8: the attention output arrives as MXFP8 (its scales reuse xn_s, free until norm2)
     GemmEpi e2{ly.proj_b, w.x, D, 0, 1, last ? 1 : 0, last ? N : 0, 0, 0, mp ? w.xn_s : nullptr,

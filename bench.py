@@ -57,6 +57,9 @@ def parse():
                     help="GPT-2 decoder arithmetic: auto = bf16 for --precision bf16 / fp8, fp32 for fp32; fp32 with "
                          "--precision bf16 is the reference's own split (ViT under half-precision autocast, "
                          "src/models/video_encoder.py:261-264; the decoder in fp32, text_decoder.py:131-144)")
+    ap.add_argument("--lm-screen", default="on", choices=["on", "off"],
+                    help="f32 decoder greedy steps: bf16 lm_head screen + exact f32 rescoring of the tokens it "
+                         "cannot rule out (on, same ids) or the f32 lm_head (off)")
     ap.add_argument("--mx-gemms", default="qkv,proj,fc1,fc2",
                     help="--precision fp8: the ViT block GEMMs run in MXFP8 (the others bf16)")
     ap.add_argument("--decode", default="hf_greedy", choices=["hf_greedy", "raw_greedy"])
@@ -557,7 +560,7 @@ def main():
     pre = HipPrefix(sd, ga.n_embd, device=dev)
     if args.dec_precision == "auto":
         args.dec_precision = "fp32" if args.precision == "fp32" else "bf16"
-    dec = HipGPT2Decoder(sd, ga, args.dec_precision, dev)
+    dec = HipGPT2Decoder(sd, ga, args.dec_precision, dev, screen=args.lm_screen == "on")
     if args.decode == "hf_greedy":
         cfg = GenConfig(args.max_new, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, not args.no_graph,
                         num_beams=args.beams)
@@ -769,6 +772,9 @@ def main():
                        "frames": T, "max_new_tokens": args.max_new,
                        "decode": args.decode if args.beams == 1 else f"beam-{args.beams} (device beam search, HF _beam_search)",
                        "vit_precision": args.precision, "decoder_precision": args.dec_precision,
+                       "lm_head": ("bf16 screen + exact f32 rescoring" if dec.screen and args.beams == 1
+                                   and args.decode == "hf_greedy" or dec.screen and args.decode == "raw_greedy"
+                                   else args.dec_precision),
                        "hipgraph_decode": not args.no_graph, "parallelism": f"dp{world}",
                        "decode_block_cap": cfg.max_blocks,
                        "schedule": "serial" if args.serial else

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 12
+#define VCAP_ABI_VERSION 13
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -107,6 +107,14 @@ typedef struct vcap_gpt2_desc {
   const float* wpe;          /* [n_positions, E] f32 */
   const float* lnf_g; const float* lnf_b;
   const vcap_gpt2_layer* layers; /* host array of n_layer entries */
+  /* f32 decoders, optional (NULL / 0 disable): a bf16 rows-packed copy of the lm_head and
+   * screen_bound = c * max_v ||w_v||_2 (c = 0.0043 covers the bf16 rounding of h and w and both
+   * f32 dot products over n_embd <= 1024).  A greedy step without requested logits then runs the
+   * lm_head in bf16 as a screen and rescores, in f32 against wte, every token whose exact score
+   * could reach the screen's maximum: the token is the exact f32 argmax (processors applied, ties
+   * to the lowest id) at half the lm_head's weight bytes. */
+  const void* lm_head_screen;
+  float screen_bound;
 } vcap_gpt2_desc;
 
 typedef struct vcap_gen_params {

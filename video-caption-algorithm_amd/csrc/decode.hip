@@ -855,15 +855,22 @@ __global__ void vcap_decode_init_kernel(int* page_table, int B, int maxp, int* f
 // Reduce the per-workgroup argmax partials, apply EOS padding, record the token, precompute the
 // n-gram ban list for the next step (one thread per n-gram start, history staged in LDS) and
 // write the next input embedding wte[tok] + wpe[pos].
-template <typename T>
+// SCREEN (f32 decoders, greedy): the partials are those of the bf16 screen (ScreenArgs); the token is
+// the exact-f32 argmax over the tokens the screen's error bound cannot rule out.
+template <typename T, bool SCREEN>
 __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
     const float* __restrict__ part_val, const int* __restrict__ part_idx, int nblk, int step, int* finished,
     int* hist, int hist_ld, int* banned, int* nbanned, int ngram, int eos, int pad, int* out_ids, int out_ld,
-    const T* __restrict__ wte, const float* __restrict__ wpe, float* __restrict__ h, int E, int pos_next, int vocab) {
+    const T* __restrict__ wte, const float* __restrict__ wpe, float* __restrict__ h, int E, int pos_next, int vocab,
+    ScreenArgs sc) {
   __shared__ float sv[4];
   __shared__ int si[4];
   __shared__ int s_h[1024];
   __shared__ int s_tok, s_nb;
+  __shared__ __attribute__((aligned(16))) float s_hf[SCREEN ? 1024 : 4];
+  __shared__ float s_red[4];
+  __shared__ int s_cb[SCREEN ? 64 : 1], s_cv[SCREEN ? 1024 : 1], s_bn[SCREEN ? 256 : 1];
+  __shared__ int s_ncb, s_ncv;
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // every load of the first phase issued at once (clamped addresses, selects after): the history,
   // the argmax partials (nblk <= 1024) and the row's finished flag
@@ -879,9 +886,21 @@ __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
     pi[q] = part_idx[(long)m * nblk + b];
   }
   const int fin = finished[m];
+  // screen: the row's ln_f output, the current ban list and its length, issued with the rest
+  f32x4 shv = (f32x4){0.f, 0.f, 0.f, 0.f};
+  int bnv = 0, nbc = 0;
+  if constexpr (SCREEN) {
+    if (tid * 4 < E) shv = *reinterpret_cast<const f32x4*>(sc.sh + (long)m * E + tid * 4);
+    bnv = banned[m * hist_ld + min(tid, hist_ld - 1)];
+    nbc = nbanned[m];
+  }
 #pragma unroll
   for (int q = 0; q < HP; ++q)
     if (tid + q * 256 < step) s_h[tid + q * 256] = hv[q];
+  if constexpr (SCREEN) {
+    if (tid * 4 < E) *reinterpret_cast<f32x4*>(s_hf + tid * 4) = shv;
+    if (tid < hist_ld) s_bn[tid] = bnv;
+  }
   float bv = -INFINITY;
   int bi = 0x7fffffff;
 #pragma unroll
@@ -893,6 +912,77 @@ __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
     si[wave] = bi;
   }
   __syncthreads();
+  if constexpr (SCREEN) {
+    float pb = sv[0];
+    int pbi = si[0];
+    for (int w = 1; w < 4; ++w) argmax_take(pb, pbi, sv[w], si[w]);
+    if (!fin && pb > -INFINITY) {
+      // ||h|| of the row's ln_f output (the f32 rows the screen's bf16 A operand was rounded from)
+      float nh = wave_sum(sumsq4(shv));
+      if (lane == 0) s_red[wave] = nh;
+      __syncthreads();
+      nh = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+      const float bmax = sc.coef * sqrtf(nh) * 1.001f;
+      const float thr = pb - 2.f * bmax;  // a token below it cannot reach the max's lower bound
+      float ev = -INFINITY;
+      int ei = 0x7fffffff;
+      const long prow = (long)m * vocab;
+      // blocks whose approximate maximum reaches the threshold (partials already in registers)
+      if (tid == 0) s_ncb = 0;
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < PP; ++q)
+        if (tid + q * 256 < nblk && pv[q] >= thr) s_cb[min(atomicAdd(&s_ncb, 1), 63)] = tid + q * 256;
+      __syncthreads();
+      const int ncb = s_ncb;
+      // the surviving columns of the candidate blocks into s_cv, 1024 column positions per pass (a
+      // candidate block holds tpb * 16 <= 512 columns: one pass for up to 2-4 candidate blocks);
+      // past 64 candidate blocks every block is scanned
+      const bool all_blocks = ncb > 64;
+      const int nsb = all_blocks ? nblk : ncb, span = sc.tpb * 16;
+      for (int from = 0; from < nsb * span; from += 1024) {
+        if (tid == 0) s_ncv = 0;
+        __syncthreads();
+        for (int i = from + tid; i < min(from + 1024, nsb * span); i += 256) {
+          const int bl = i / span, off = i - bl * span;
+          const int v = (all_blocks ? bl : s_cb[bl]) * span + off;
+          if (v < vocab && sc.proc[prow + v] >= thr) s_cv[atomicAdd(&s_ncv, 1)] = v;
+        }
+        __syncthreads();
+        const int ncv = s_ncv;
+        for (int i = wave; i < ncv; i += 4) {
+          const int vv = s_cv[i];
+          float d = 0.f;
+          for (int c = lane * 4; c < E; c += 256) {
+            const f32x4 w4 = *reinterpret_cast<const f32x4*>(sc.w32 + (long)vv * E + c);
+            const f32x4 h4 = *reinterpret_cast<const f32x4*>(s_hf + c);
+            d = fmaf(w4.w, h4.w, fmaf(w4.z, h4.z, fmaf(w4.y, h4.y, fmaf(w4.x, h4.x, d))));
+          }
+          float p = wave_sum(d);
+          // RepetitionPenalty -> NoRepeatNGram -> MinNewTokens, the lm_head epilogue's order
+          if (sc.rep != 1.0f) {
+            bool rep_hit = false;
+            for (int t = 0; t < step; ++t) rep_hit |= s_h[t] == vv;
+            if (rep_hit) p = p < 0.f ? p * sc.rep : p / sc.rep;
+          }
+          bool ban_hit = false;
+          for (int t = 0; t < nbc; ++t) ban_hit |= s_bn[t] == vv;
+          if (ban_hit) p = -INFINITY;
+          if (vv == eos && step < sc.min_new) p = -INFINITY;
+          argmax_take(ev, ei, p, vv);
+        }
+        __syncthreads();  // s_cv / s_ncv reused by the next pass
+      }
+      __syncthreads();  // s_red reads done
+      if (lane == 0) {
+        sv[wave] = ev;
+        si[wave] = ei;
+      }
+      __syncthreads();
+      bv = sv[0];
+      bi = si[0];
+    }
+  }
   if (tid == 0) {
     for (int w = 1; w < 4; ++w) argmax_take(bv, bi, sv[w], si[w]);
     int tok = bi;
@@ -1090,6 +1180,8 @@ __global__ __launch_bounds__(256) void vcap_lm_head_stream_kernel(RowsGemmArgs a
     for (int c = 0; c < KC; ++c) {
       if (c * 256 + lane * 4 < K) {
         const f32x4 y = live ? ln_affine4(xv[r][c], mean, rstd, gv[c], bv[c]) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (a.screen_h && blockIdx.x == 0 && live)
+          *reinterpret_cast<f32x4*>(a.screen_h + (long)m * K + c * 256 + lane * 4) = y;
         const int byte = (c * 256 + lane * 4) * (int)sizeof(T);
         char* dst = dyn + (long)m * (K * (int)sizeof(T)) + ((((byte >> 4) ^ (m & 15))) << 4) + (byte & 15);
         if constexpr (sizeof(T) == 2) {
@@ -1168,7 +1260,8 @@ __global__ __launch_bounds__(256) void vcap_lm_head_stream_kernel(RowsGemmArgs a
 }
 
 template <typename T, int NSL>
-static bool launch_lm_stream(const RowsGemmArgs& a, int* nblk_out, hipStream_t s, hipError_t& err) {
+static bool launch_lm_stream(const RowsGemmArgs& a, int* nblk_out, hipStream_t s, hipError_t& err,
+                             int* tpb_out = nullptr) {
   constexpr int NTB = (NSL <= 8) ? 4 : 2;  // two register sets of NSL x NTB fragments
   const int ntiles = (a.N + 15) / 16;
   const int cus = vcap_device_cus();
@@ -1181,6 +1274,7 @@ static bool launch_lm_stream(const RowsGemmArgs& a, int* nblk_out, hipStream_t s
   const int grid = (ntiles + tpw - 1) / tpw;
   hipLaunchKernelGGL((vcap_lm_head_stream_kernel<T, NSL, NTB>), dim3(grid), dim3(256), lds, s, a, tpw);
   if (nblk_out) *nblk_out = grid;
+  if (tpb_out) *tpb_out = tpw;
   err = hipGetLastError();
   return true;
 }
@@ -1199,6 +1293,16 @@ static bool try_lm_stream(int dt, const RowsGemmArgs& a, int* nblk_out, hipStrea
   }
 #undef VCAP_LMS
   return false;
+}
+
+hipError_t vcap_lm_head_screen_dispatch(const RowsGemmArgs& a, int* nblk_out, int* tpb_out, hipStream_t s) {
+  if (a.M > 16 || a.hist_ld > 64 || (a.K != 768 && a.K != 1024) || !a.screen_h || !a.proc_out)
+    return hipErrorNotSupported;
+  if ((long)a.M * a.ldx * 4 >= 0x7FFFFFFFL) return hipErrorNotSupported;
+  hipError_t err = hipSuccess;
+  const bool ok = a.K == 768 ? launch_lm_stream<bf16_t, 6>(a, nblk_out, s, err, tpb_out)
+                             : launch_lm_stream<bf16_t, 8>(a, nblk_out, s, err, tpb_out);
+  return ok ? err : hipErrorNotSupported;
 }
 
 // 16-column tiles per workgroup: the lm_head always takes 4 (argmax partials per 64 columns; 786
@@ -1377,15 +1481,27 @@ hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* fini
 hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const int* part_idx, int nblk, int B,
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,
-                                         const float* wpe, float* h, int E, int pos_next, int vocab, hipStream_t s) {
+                                         const float* wpe, float* h, int E, int pos_next, int vocab, hipStream_t s,
+                                         const ScreenArgs* screen) {
   if (hist_ld > 1024 || nblk < 1 || nblk > 2048 || step >= hist_ld) return hipErrorInvalidValue;
+  ScreenArgs sc{};
+  if (screen) {
+    if (dt != VCAP_DT_F32 || E > 1024 || E % 4 || hist_ld > 256 || screen->tpb < 1 || !screen->proc || !screen->sh ||
+        !screen->w32)
+      return hipErrorInvalidValue;
+    sc = *screen;
+  }
   if (dt == VCAP_DT_BF16)
-    hipLaunchKernelGGL((vcap_decode_finalize_kernel<bf16_t>), dim3(B), dim3(256), 0, s, part_val, part_idx, nblk,
-                       step, finished, hist, hist_ld, banned, nbanned, ngram, eos, pad, out_ids, out_ld,
-                       (const bf16_t*)wte, wpe, h, E, pos_next, vocab);
+    hipLaunchKernelGGL((vcap_decode_finalize_kernel<bf16_t, false>), dim3(B), dim3(256), 0, s, part_val, part_idx,
+                       nblk, step, finished, hist, hist_ld, banned, nbanned, ngram, eos, pad, out_ids, out_ld,
+                       (const bf16_t*)wte, wpe, h, E, pos_next, vocab, sc);
+  else if (screen)
+    hipLaunchKernelGGL((vcap_decode_finalize_kernel<float, true>), dim3(B), dim3(256), 0, s, part_val, part_idx,
+                       nblk, step, finished, hist, hist_ld, banned, nbanned, ngram, eos, pad, out_ids, out_ld,
+                       (const float*)wte, wpe, h, E, pos_next, vocab, sc);
   else
-    hipLaunchKernelGGL((vcap_decode_finalize_kernel<float>), dim3(B), dim3(256), 0, s, part_val, part_idx, nblk,
-                       step, finished, hist, hist_ld, banned, nbanned, ngram, eos, pad, out_ids, out_ld,
-                       (const float*)wte, wpe, h, E, pos_next, vocab);
+    hipLaunchKernelGGL((vcap_decode_finalize_kernel<float, false>), dim3(B), dim3(256), 0, s, part_val, part_idx,
+                       nblk, step, finished, hist, hist_ld, banned, nbanned, ngram, eos, pad, out_ids, out_ld,
+                       (const float*)wte, wpe, h, E, pos_next, vocab, sc);
   return hipGetLastError();
 }

@@ -161,6 +161,7 @@ int check_vit(const vcap_vit_desc* d) {
 // ----------------------------------------------------------------------------------- GPT-2
 struct DecBufs {
   float* h;
+  float* sh;  // [B][E] f32 ln_f rows of the bf16 lm_head screen (f32 greedy)
   void* q;
   void* attn;
   void* act;
@@ -205,6 +206,7 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.nbanned = (int*)c.take((size_t)B * 4);
   b.finished = (int*)c.take((size_t)B * 4);
   b.proc = (float*)c.take((size_t)B * d->vocab * 4);
+  b.sh = (float*)c.take((size_t)B * E * 4);
   b.seed = (unsigned*)c.take(8);
   return b;
 }
@@ -315,10 +317,37 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
     const int past = step == 0 ? 0 : S0 + step - 1;
     if (int rc = run_layers(d, w, maxp, page_elems, B * S_new, S_new, past, gp->max_blocks, s)) return rc;
     int nblk = 0;
-    if (int rc = run_lm_head(d, w, B, S_new, logits_out ? logits_out + (size_t)step * B * V : nullptr, max_new, step,
-                             gp->repetition_penalty, gp->min_new_tokens, gp->eos_token_id, &nblk, s,
-                             sp ? w.proc : nullptr))
-      return rc;
+    // f32 greedy: the bf16 lm_head screens, the finalize rescores the survivors in f32 (exact argmax);
+    // requested raw logits or sampling need every f32 score - the f32 lm_head then
+    ScreenArgs sc{};
+    bool screen = false;
+    if (dt == VCAP_DT_F32 && d->lm_head_screen && d->screen_bound > 0.f && !logits_out && !sp) {
+      RowsGemmArgs g;
+      memset(&g, 0, sizeof(g));
+      g.M = B; g.x = w.h + (size_t)(S_new - 1) * E; g.ldx = (long)S_new * E;
+      g.ln_g = d->lnf_g; g.ln_b = d->lnf_b; g.ln_eps = d->ln_eps;
+      g.w = d->lm_head_screen; g.N = V; g.K = E;
+      g.part_val = w.pval; g.part_idx = w.pidx;
+      g.hist = w.hist; g.hist_ld = max_new; g.gen_len = step; g.banned = w.banned; g.nbanned = w.nbanned;
+      g.rep_penalty = gp->repetition_penalty; g.min_new = gp->min_new_tokens; g.eos = gp->eos_token_id;
+      g.proc_out = w.proc; g.screen_h = w.sh;
+      int tpb = 0;
+      const hipError_t e = vcap_lm_head_screen_dispatch(g, &nblk, &tpb, s);
+      if (e == hipSuccess) {
+        const float rep = gp->repetition_penalty;
+        const float pfac = rep >= 1.f ? rep : 1.f / rep;
+        sc = ScreenArgs{w.proc, w.sh, (const float*)d->wte, d->screen_bound * pfac, tpb, rep, gp->min_new_tokens};
+        screen = true;
+      } else if (e != hipErrorNotSupported) {
+        return hip_fail(e, "lm_head_screen");
+      }
+    }
+    if (!screen) {
+      if (int rc = run_lm_head(d, w, B, S_new, logits_out ? logits_out + (size_t)step * B * V : nullptr, max_new,
+                               step, gp->repetition_penalty, gp->min_new_tokens, gp->eos_token_id, &nblk, s,
+                               sp ? w.proc : nullptr))
+        return rc;
+    }
     if (sp) {
       SampleArgs sa{w.proc, V, V, sp->temperature, sp->top_k, sp->top_p, w.seed, step, force_ids, max_new,
                     warped_out ? warped_out + (size_t)step * B * V : nullptr, V, w.pval, w.pidx,
@@ -329,7 +358,8 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
     VCAP_TRY(vcap_decode_finalize_dispatch(dt, w.pval, w.pidx, nblk, B, step, w.finished, w.hist, max_new, w.banned,
                                            w.nbanned, gp->no_repeat_ngram_size, gp->eos_token_id, gp->pad_token_id,
                                            out_ids, max_new, d->wte, d->wpe, w.h, E,
-                                           (S0 + step) < d->n_positions ? S0 + step : d->n_positions - 1, V, s),
+                                           (S0 + step) < d->n_positions ? S0 + step : d->n_positions - 1, V, s,
+                                           screen ? &sc : nullptr),
              "finalize");
   }
   return 0;

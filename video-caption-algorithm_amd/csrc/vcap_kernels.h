@@ -63,6 +63,23 @@ struct RowsGemmArgs {
   int max_blocks;  // 0: one 16-column tile per workgroup; > 0: widen tiles to stay near this grid
   float* proc_out;  // EPI_LOGITS, optional [M, N]: the processed scores (sampling mode)
   int half;         // set by vcap_rows_gemm_dispatch: residual GEMV tiles split into two 8-column workgroups
+  float* screen_h;  // lm_head stream kernel, optional [M, K] f32: workgroup 0 stores the ln_f rows it used
+};
+
+// Exact-fp32 greedy token from a bf16 lm_head screen (f32 decoders; vcap_decode_finalize_dispatch):
+// the bf16 stream kernel left the processed approximate scores in `proc` [B][vocab], its argmax
+// partials per block of `tpb` 16-column tiles, and the f32 ln_f rows in `sh` [B][E].  Every token
+// whose exact f32 processed score could reach the approximate maximum's lower bound (|approx - exact|
+// <= coef * ||h||, coef = c * max_v ||w_v|| * max(rep, 1 / rep)) is rescored against the f32 `w32`
+// rows; the argmax of the exact scores (value, then lowest index) is the token.
+struct ScreenArgs {
+  const float* proc;
+  const float* sh;
+  const float* w32;
+  float coef;
+  int tpb;
+  float rep;
+  int min_new;
 };
 
 // ---- sampling warpers + draw (csrc/sample.hip)
@@ -134,7 +151,11 @@ hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* fini
 hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const int* part_idx, int nblk, int B,
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,
-                                         const float* wpe, float* h, int E, int pos_next, int vocab, hipStream_t s);
+                                         const float* wpe, float* h, int E, int pos_next, int vocab, hipStream_t s,
+                                         const ScreenArgs* screen = nullptr);
+// The bf16 lm_head as the screen of an f32 greedy step (the stream kernel only: M <= 16); returns
+// hipErrorNotSupported, launching nothing, where that kernel does not apply.
+hipError_t vcap_lm_head_screen_dispatch(const RowsGemmArgs& a, int* nblk_out, int* tpb_out, hipStream_t s);
 hipError_t vcap_embed_tokens_dispatch(int dt, const int* tok, int rows, const void* wte, const float* wpe, float* h,
                                       int E, int pos, hipStream_t s);
 // ---- device beam search (csrc/beam.hip) ----

@@ -16,7 +16,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
 DT_F32, DT_BF16, DT_MXFP8 = 0, 1, 2
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
@@ -57,7 +57,8 @@ class GPT2Layer(C.Structure):
 class GPT2Desc(C.Structure):
     _fields_ = [("dtype", i32), ("n_embd", i32), ("n_layer", i32), ("n_head", i32), ("vocab", i32),
                 ("n_positions", i32), ("prefix_len", i32), ("ln_eps", f32), ("wte", vp), ("lm_head", vp), ("wpe", vp),
-                ("lnf_g", vp), ("lnf_b", vp), ("layers", C.POINTER(GPT2Layer))]
+                ("lnf_g", vp), ("lnf_b", vp), ("layers", C.POINTER(GPT2Layer)), ("lm_head_screen", vp),
+                ("screen_bound", f32)]
 
 
 class GenParams(C.Structure):

@@ -233,8 +233,16 @@ class GenConfig:
 class HipGPT2Decoder:
     """GPT2LMHeadModel greedy generate from inputs_embeds (text_decoder.py:131-144) on the HIP path."""
 
+    # |bf16-screen score - exact f32 score| <= SCREEN_C * ||h||_2 * ||w_v||_2: 2^-8 (+ the squared term)
+    # for rounding h and w to bf16, 2 x 1024 x 2^-24 for the two f32 dot products (n_embd <= 1024):
+    # 0.00403, and 6 % over it (an MFMA accumulating with truncation doubles the dot-product terms)
+    SCREEN_C = 0.0043
+
     def __init__(self, sd: Dict[str, np.ndarray], arch: GPT2Arch, precision: str = "bf16", device="cuda",
-                 prefix_len: int = 4):
+                 prefix_len: int = 4, screen: bool = True):
+        """precision "fp32" with `screen`: a greedy step without requested logits runs the lm_head
+        in bf16 as a screen and rescores the tokens it cannot rule out in f32 (csrc/decode.hip,
+        vcap_decode_finalize_kernel<float, true>): the same exact-f32 argmax for half the bytes."""
         N.lib()
         self.arch, self.precision, self.device = arch, precision, torch.device(device)
         self.dt, tdt = _dtype(precision)
@@ -256,6 +264,12 @@ class HipGPT2Decoder:
         self.wte = self.wte.contiguous()
         self._keep.append(self.wte)
         self.lm_head = self._pack(self.wte)   # tied lm_head, packed copy
+        screen_w, screen_bound = None, 0.0
+        if self.dt == N.DT_F32 and screen:
+            screen_w = self._pack(self.wte.to(torch.bfloat16).contiguous(), N.DT_BF16)
+            wmax = float(torch.linalg.vector_norm(self.wte.double(), dim=1).max())
+            screen_bound = self.SCREEN_C * wmax * (1.0 + 1e-6)
+        self.screen = screen_w is not None
         self.wpe = f32(p + "wpe.weight")
         lnf_g, lnf_b = f32(p + "ln_f.weight"), f32(p + "ln_f.bias")
         self.layers = (N.GPT2Layer * arch.n_layer)()
@@ -274,19 +288,22 @@ class HipGPT2Decoder:
                                vocab=arch.vocab, n_positions=arch.n_positions, prefix_len=prefix_len,
                                ln_eps=arch.ln_eps, wte=self.wte.data_ptr(), lm_head=self.lm_head.data_ptr(),
                                wpe=self.wpe.data_ptr(),
-                               lnf_g=lnf_g.data_ptr(), lnf_b=lnf_b.data_ptr(), layers=self.layers)
+                               lnf_g=lnf_g.data_ptr(), lnf_b=lnf_b.data_ptr(), layers=self.layers,
+                               lm_head_screen=screen_w.data_ptr() if screen_w is not None else None,
+                               screen_bound=screen_bound)
         self.ws = _Workspace(dev)
         self._stable = {}             # (B, max_new) -> persistent prefix / ids buffers (graph reuse)
         torch.cuda.synchronize(dev)   # packing ran on the current stream; decodes may use others
 
-    def _pack(self, w: torch.Tensor) -> torch.Tensor:
+    def _pack(self, w: torch.Tensor, dt: Optional[int] = None) -> torch.Tensor:
         """[N, K] device weight -> rows-packed copy (MFMA-fragment order, csrc/decode.hip)."""
+        dt = self.dt if dt is None else dt
         rows, k = w.shape
-        nbytes = int(N.lib().vcap_rows_packed_bytes(self.dt, rows, k))
+        nbytes = int(N.lib().vcap_rows_packed_bytes(dt, rows, k))
         if nbytes == 0:
             raise ValueError(f"cannot pack a [{rows}, {k}] weight (K must be a multiple of 32 bf16 / 16 f32)")
         packed = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
-        N.check(N.lib().vcap_rows_pack(self.dt, w.data_ptr(), w.stride(0), rows, k, packed.data_ptr(),
+        N.check(N.lib().vcap_rows_pack(dt, w.data_ptr(), w.stride(0), rows, k, packed.data_ptr(),
                                        _stream(w.device)), "vcap_rows_pack")
         self._keep.append(packed)
         return packed

@@ -485,7 +485,12 @@ __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int M = a.M, N = a.N;
-  const int n0 = blockIdx.x * 16;
+  // a.half: two workgroups per 16-column tile, each streaming 8 columns' weights (as in
+  // vcap_rows_gemv_kernel: lanes l and l ^ 8 load the same fragment), the stores of its 8 columns
+  const bool half = a.half != 0;
+  const int hsel = half ? (int)(blockIdx.x & 1) : -1;
+  const int n0 = half ? (int)(blockIdx.x >> 1) * 16 : (int)blockIdx.x * 16;
+  const int wlane = half ? ((lane & 0x30) | (hsel << 3) | (lane & 7)) : lane;
   const int nslab = 8 * NSL, g0 = wave * NSL;
   const int ntiles = (N + 15) >> 4;
   u32x4 af[NSL];
@@ -494,7 +499,7 @@ __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
   for (int s = 0; s < NSL; ++s) af[s] = vcap_dec_aload(a.x, (xo + (g0 + s) * KS) * (long)sizeof(T));
   asm volatile("" ::: "memory");  // the activation loads issue before the weights
   u32x4 wf[NSL];
-  const u32x4* wp = packed_frag(a.w, min((int)blockIdx.x, ntiles - 1), nslab, g0, lane);
+  const u32x4* wp = packed_frag(a.w, min(n0 / 16, ntiles - 1), nslab, g0, wlane);
 #pragma unroll
   for (int s = 0; s < NSL; ++s) wf[s] = vcap_dec_wload<true>(a.w, wp + s * 64);
   const int row = (tid >> 4) & 15, col = tid & 15;
@@ -509,7 +514,7 @@ __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wave][(fg * 4 + r) * 16 + fr] = acc[r];
   __syncthreads();
-  if (tid < 256 && row < M && n0 + col < N) {
+  if (tid < 256 && row < M && n0 + col < N && (hsel < 0 || (col >> 3) == hsel)) {
     const int e = tid;
     const float v = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) +
                     ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e])) + pre_bias;
@@ -1090,7 +1095,8 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
     return err;
   if constexpr (sizeof(T) == 4 && MT == 1 && NTB == 1 && PRO == PRO_DIRECT && EPI == EPI_RESID) {
     if (nsl == 48) {  // f32 mlp c_proj of GPT-2 small (K = 3072): 8 waves x 24 slabs
-      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 24>), dim3((a.N + 15) / 16), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 24>), dim3((a.half ? 2 : 1) * ((a.N + 15) / 16)), dim3(512),
+                         0, s, a);
       return hipGetLastError();
     }
   }

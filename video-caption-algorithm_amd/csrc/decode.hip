@@ -284,6 +284,73 @@ VCAP_DEV void c64_finish(const C64Loads& L, float* s_q, float* s_p, int ctx, bf1
   }
 }
 
+// The f32 form (the f32 decoders): the same item on one wave with every load issued at once; the
+// score sums dims 0..63 in order and the P.V sums run over the same key groups and DPP / permlane
+// reduction as vcap_decode_attention_kernel<float>.
+struct C64LoadsF {
+  u32x4 q;       // 4 of the head's 64 query dims: chunk (lane & 15)
+  u32x4 kv[16];  // K row of key min(lane, ctx - 1)
+  u32x4 vv[8][2];  // V rows of keys it * 8 + kg (clamped), dims [d8, d8 + 8)
+};
+
+VCAP_DEV void c64f_issue(C64LoadsF& L, const float* q, const float* kc, const float* vc, int maxp, int m, int h,
+                         int H, int seq, int ctx) {
+  const int lane = threadIdx.x & 63, kg = lane >> 3, d8 = (lane & 7) * 8;
+  auto row_of = [&](int j) { return (((long)(seq * maxp + (j >> 4)) * H + h) * 16 + (j & 15)) * 64; };
+  auto ld = [](const float* base, long elem) { return *reinterpret_cast<const u32x4*>(base + elem); };
+  L.q = ld(q, (long)m * H * 64 + h * 64 + (lane & 15) * 4);
+  const long kr = row_of(min(lane, ctx - 1));
+#pragma unroll
+  for (int c = 0; c < 16; ++c) L.kv[c] = ld(kc, kr + c * 4);
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const long vr = row_of(min(it * 8 + kg, ctx - 1)) + d8;
+    L.vv[it][0] = ld(vc, vr);
+    L.vv[it][1] = ld(vc, vr + 4);
+  }
+}
+
+VCAP_DEV void c64f_finish(const C64LoadsF& L, float* s_q, float* s_p, int ctx, float* orow) {
+  const int lane = threadIdx.x & 63, kg = lane >> 3, d8 = (lane & 7) * 8;
+  if (lane < 16) *reinterpret_cast<f32x4*>(s_q + lane * 4) = __builtin_bit_cast(f32x4, L.q);
+  __builtin_amdgcn_wave_barrier();
+  float sc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const f32x4 k4 = __builtin_bit_cast(f32x4, L.kv[c]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sc += s_q[c * 4 + e] * k4[e];
+  }
+  sc *= 0.125f;
+  const bool live = lane < ctx;
+  const float mx = wave_max(live ? sc : -INFINITY);
+  const float p = live ? __expf(sc - mx) : 0.f;
+  const float sum = wave_sum(p);
+  s_p[lane] = p;
+  __builtin_amdgcn_wave_barrier();
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = 0.f;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int jj = it * 8 + kg;
+    const float pj = jj < ctx ? s_p[jj] : 0.f;
+    const f32x4 v0 = __builtin_bit_cast(f32x4, L.vv[it][0]), v1 = __builtin_bit_cast(f32x4, L.vv[it][1]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] += pj * v0[e];
+      o[4 + e] += pj * v1[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = rows_sum(o[e] + dpp_f<0x128>(o[e]));
+  if (kg == 0) {
+    const float inv = 1.0f / sum;
+    *reinterpret_cast<f32x4*>(orow + d8) = (f32x4){o[0], o[1], o[2], o[3]} * inv;
+    *reinterpret_cast<f32x4*>(orow + d8 + 4) = (f32x4){o[4], o[5], o[6], o[7]} * inv;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Decode GEMV (M <= 32 rows): everything a workgroup needs from memory is issued at kernel start,
 // in the order it is consumed (vmcnt retires in issue order):
@@ -1417,6 +1484,23 @@ __global__ __launch_bounds__(64) void vcap_decode_attention_c64_kernel(const bf1
   c64_finish(L, s_q, s_p, ctx, out + (long)m * H * 64 + h * 64);
 }
 
+__global__ __launch_bounds__(64) void vcap_decode_attention_c64f_kernel(const float* __restrict__ q,
+                                                                        const float* __restrict__ kc,
+                                                                        const float* __restrict__ vc, int maxp,
+                                                                        float* __restrict__ out, int M, int H,
+                                                                        int S_new, int past) {
+  __shared__ __attribute__((aligned(16))) float s_q[64];
+  __shared__ float s_p[64];
+  const int item = blockIdx.x;
+  if (item >= M * H) return;
+  const int m = item / H, h = item - m * H;
+  const int seq = m / S_new, qpos = past + (m - seq * S_new);
+  const int ctx = qpos + 1;  // <= 64 (dispatcher)
+  C64LoadsF L;
+  c64f_issue(L, q, kc, vc, maxp, m, h, H, seq, ctx);
+  c64f_finish(L, s_q, s_p, ctx, out + (long)m * H * 64 + h * 64);
+}
+
 hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc, const void* vc, const int* pt,
                                           int maxp, void* out, int M, int H, int S_new, int past, hipStream_t s) {
   if (past + S_new > 1024 || maxp > 64) return hipErrorInvalidValue;
@@ -1426,6 +1510,11 @@ hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc,
     // many CUs (each item's q / K / V round trip on a CU of its own) instead of 4 per CU
     hipLaunchKernelGGL(vcap_decode_attention_c64_kernel, dim3(M * H), dim3(64), 0, s, (const bf16_t*)q,
                        (const bf16_t*)kc, (const bf16_t*)vc, maxp, (bf16_t*)out, M, H, S_new, past);
+    return hipGetLastError();
+  }
+  if (dt == VCAP_DT_F32 && !pt && past + S_new <= 64) {
+    hipLaunchKernelGGL(vcap_decode_attention_c64f_kernel, dim3(M * H), dim3(64), 0, s, (const float*)q,
+                       (const float*)kc, (const float*)vc, maxp, (float*)out, M, H, S_new, past);
     return hipGetLastError();
   }
   if (!pt) return hipErrorInvalidValue;  // the general kernels read the page table

@@ -250,9 +250,9 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     a.page_table = nullptr; a.maxp = maxp; a.H = H; a.S_new = S_new; a.past = past; a.max_blocks = max_blocks;
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_LN, EPI_QKV, a, nullptr, s), "c_attn");
     // 2) causal attention over the paged cache
-    // pages are allocated contiguously per sequence (vcap_decode_init: identity table), so the bf16
-    // short-context kernel computes page ids instead of loading them (nullptr table)
-    const int* pt_arg = (dt == VCAP_DT_BF16 && past + S_new <= 64) ? nullptr : w.pt;
+    // pages are allocated contiguously per sequence (vcap_decode_init: identity table), so the
+    // short-context kernels (bf16 and f32) compute page ids instead of loading them (nullptr table)
+    const int* pt_arg = past + S_new <= 64 ? nullptr : w.pt;
     if (anc)   // beam search: keys through the ancestry table (one query row per sequence)
       VCAP_TRY(vcap_decode_attention_anc_dispatch(dt, w.q, a.kc, a.vc, anc, anc_ld, maxp, w.attn, M, H, past, s),
                "decode_attention_anc");

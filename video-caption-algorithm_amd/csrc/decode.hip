@@ -1015,20 +1015,33 @@ __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
       for (int from = 0; from < nsb * span; from += 1024) {
         if (tid == 0) s_ncv = 0;
         __syncthreads();
-        for (int i = from + tid; i < min(from + 1024, nsb * span); i += 256) {
+        const int lim = min(from + 1024, nsb * span);
+        int cv[4];
+        float cp[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // the four loads issued together
+          const int i = from + tid + r * 256;
           const int bl = i / span, off = i - bl * span;
-          const int v = (all_blocks ? bl : s_cb[bl]) * span + off;
-          if (v < vocab && sc.proc[prow + v] >= thr) s_cv[atomicAdd(&s_ncv, 1)] = v;
+          cv[r] = i < lim ? (all_blocks ? bl : s_cb[min(bl, 63)]) * span + off : vocab;
+          cp[r] = sc.proc[prow + min(cv[r], vocab - 1)];
         }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (cv[r] < vocab && cp[r] >= thr) s_cv[atomicAdd(&s_ncv, 1)] = cv[r];
         __syncthreads();
         const int ncv = s_ncv;
         for (int i = wave; i < ncv; i += 4) {
           const int vv = s_cv[i];
+          f32x4 w4[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)  // E <= 1024: the row's loads issued together
+            w4[r] = *reinterpret_cast<const f32x4*>(sc.w32 + (long)vv * E + min(lane * 4 + r * 256, E - 4));
           float d = 0.f;
-          for (int c = lane * 4; c < E; c += 256) {
-            const f32x4 w4 = *reinterpret_cast<const f32x4*>(sc.w32 + (long)vv * E + c);
-            const f32x4 h4 = *reinterpret_cast<const f32x4*>(s_hf + c);
-            d = fmaf(w4.w, h4.w, fmaf(w4.z, h4.z, fmaf(w4.y, h4.y, fmaf(w4.x, h4.x, d))));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (lane * 4 + r * 256 >= E) break;
+            const f32x4 h4 = *reinterpret_cast<const f32x4*>(s_hf + lane * 4 + r * 256);
+            d = fmaf(w4[r].w, h4.w, fmaf(w4[r].z, h4.z, fmaf(w4[r].y, h4.y, fmaf(w4[r].x, h4.x, d))));
           }
           float p = wave_sum(d);
           // RepetitionPenalty -> NoRepeatNGram -> MinNewTokens, the lm_head epilogue's order

@@ -177,6 +177,13 @@ __global__ __launch_bounds__(256) void vcap_beam_cand_kernel(BeamState st, const
   }
 }
 
+// candidates per lane of the select kernel: a GPT-2 vocabulary's 25 chunks of top-2nb per beam
+// (NB = 4: 800 -> 13 per lane), at most 20
+constexpr int select_nc(int nb) {
+  const int n = (nb * 25 * 2 * nb + 63) / 64;
+  return n < 1 ? 1 : (n > 20 ? 20 : n);
+}
+
 // register "gather": a[idx] of a small unrolled array as an OR of masked terms (a compare /
 // select chain is canonicalised back into a dynamically indexed private array = scratch memory)
 template <int NB>
@@ -195,7 +202,7 @@ template <int NB>
 __global__ __launch_bounds__(512) void vcap_beam_select_kernel(BeamState st, int B, int L, int V, int C,
                                                                 int cur, int eos, float lpen, int S0, int anc_ld) {
   constexpr int K = 2 * NB;
-  constexpr int NC = 20;   // candidates per lane (NB * C * K <= 1280)
+  constexpr int NC = select_nc(NB);   // candidates per lane (NB * C * K <= 64 * NC)
   __shared__ int s_unsat[8], s_allhits[8];
   const int lane = threadIdx.x & 63, b = threadIdx.x >> 6;
   const bool live = b < B;
@@ -229,8 +236,10 @@ __global__ __launch_bounds__(512) void vcap_beam_select_kernel(BeamState st, int
 #pragma unroll
   for (int q = 0; q < NC; ++q) {
     const int i = min(lane + q * 64, ncand - 1);
-    const int beam = i / (C * K), rest = i - beam * (C * K);
-    const long src = (long)(bl * NB + beam) * C * K + rest;
+    int beam = 0;   // i / (C * K) by compares (an integer division is ~30 VALU per candidate)
+#pragma unroll
+    for (int j = 1; j < NB; ++j) beam += i >= j * C * K;
+    const long src = (long)bl * NB * C * K + i;
     const int t = st.cand_tok[src];
     const float v = st.cand_val[src];
     const bool ok = lane + q * 64 < ncand && t < V;   // (a chunk with fewer than 2nb columns)
@@ -249,35 +258,39 @@ __global__ __launch_bounds__(512) void vcap_beam_select_kernel(BeamState st, int
   if (stopped) return;   // HF's loop has ended: no further updates (uniform)
   int hits_all = 1;
   if (live) {
-    // ---- top-2nb over the beams' chunk candidates (flat index beam * V + token, HF topk order)
+    // ---- top-2nb over the beams' chunk candidates (flat index beam * V + token, HF topk order).
+    // Branch-free: a taken candidate becomes (-inf, INT_MAX), which loses every comparison against a
+    // live one (a live -inf keeps its index); absent entries hold the same pair from the loads.
+    // (Per-lane `taken` flags and guarded takes compiled to ~7800 instructions with 300 exec-mask
+    // branches: 21-24 us per step, r05.)
     float topv[K];
     int topf[K];
-    {
-      bool taken[NC];
 #pragma unroll
-      for (int q = 0; q < NC; ++q) taken[q] = cf[q] == 0x7fffffff;
+    for (int k = 0; k < K; ++k) {
+      float bv = cv[0];
+      int bi = cf[0];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        float bv = -INFINITY;
-        int bi = 0x7fffffff;
+      for (int q = 1; q < NC; ++q) argmax_take(bv, bi, cv[q], cf[q]);
+      wave_argmax(bv, bi);
 #pragma unroll
-        for (int q = 0; q < NC; ++q)
-          if (!taken[q]) argmax_take(bv, bi, cv[q], cf[q]);
-        wave_argmax(bv, bi);
-#pragma unroll
-        for (int q = 0; q < NC; ++q)
-          if (!taken[q] && cf[q] == bi) taken[q] = true;
-        topv[k] = bv;
-        topf[k] = bi;
+      for (int q = 0; q < NC; ++q) {
+        const bool h = cf[q] == bi;
+        cv[q] = h ? -INFINITY : cv[q];
+        cf[q] = h ? 0x7fffffff : cf[q];
       }
+      topv[k] = bv;
+      topf[k] = bi;
     }
     int src_beam[K], tok[K], hit[K];
     float run_lp[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      src_beam[k] = topf[k] / V;
-      tok[k] = topf[k] - src_beam[k] * V;
-      hit[k] = (tok[k] == eos) || (cur + 1 >= L);
+      int sb = 0;   // topf / V by compares
+#pragma unroll
+      for (int j = 1; j < NB; ++j) sb += topf[k] >= j * V;
+      src_beam[k] = sb;
+      tok[k] = topf[k] - sb * V;
+      hit[k] = (tok[k] == eos) | (cur + 1 >= L);
       run_lp[k] = topv[k] + (hit[k] ? kNeg : -0.0f);   // topk_lp + hits * -1e9
       hits_all &= hit[k];
     }
@@ -291,11 +304,11 @@ __global__ __launch_bounds__(512) void vcap_beam_select_kernel(BeamState st, int
         int best = -1;
         float bv = 0.f;
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-          if (!(used >> k & 1) && (best < 0 || run_lp[k] > bv)) {
-            best = k;
-            bv = run_lp[k];
-          }
+        for (int k = 0; k < K; ++k) {
+          const bool t = !((used >> k) & 1u) & ((best < 0) | (run_lp[k] > bv));
+          best = t ? k : best;
+          bv = t ? run_lp[k] : bv;
+        }
         used |= 1u << best;
         nxt_lp[i] = bv;
         nxt_tok[i] = pick<K>(tok, best);
@@ -326,24 +339,20 @@ __global__ __launch_bounds__(512) void vcap_beam_select_kernel(BeamState st, int
         int e = -1;
         float bv = 0.f;
 #pragma unroll
-        for (int k = 0; k < NB + K; ++k)
-          if (!(used >> k & 1) && (e < 0 || msc[k] > bv)) {
-            e = k;
-            bv = msc[k];
-          }
+        for (int k = 0; k < NB + K; ++k) {
+          const bool t = !((used >> k) & 1u) & ((e < 0) | (msc[k] > bv));
+          e = t ? k : e;
+          bv = t ? msc[k] : bv;
+        }
         used |= 1u << e;
         new_bsc[i] = bv;
-        if (e < NB) {
-          new_seq[i] = pick<NB>(sq, e);
-          new_bidx[i] = pick<NB>(bix, e);
-          new_fin[i] = pick<NB>(fn, e);
-        } else {
-          const int k = e - NB;
-          const int cs = pick<K>(src_beam, k);
-          new_seq[i] = p == cur ? pick<K>(tok, k) : pick<NB>(rs, cs);
-          new_bidx[i] = p == cur ? b * NB + cs : pick<NB>(rbx, cs);
-          new_fin[i] = pick<K>(hit, k) && k < NB;
-        }
+        // an existing finished hypothesis (e < NB) or candidate k = e - NB: both formed, one kept
+        const int k = e - NB;
+        const int cs = pick<K>(src_beam, k);
+        const bool old_fin = e < NB;
+        new_seq[i] = old_fin ? pick<NB>(sq, e) : (p == cur ? pick<K>(tok, k) : pick<NB>(rs, cs));
+        new_bidx[i] = old_fin ? pick<NB>(bix, e) : (p == cur ? b * NB + cs : pick<NB>(rbx, cs));
+        new_fin[i] = old_fin ? pick<NB>(fn, e) : (pick<K>(hit, k) & (k < NB));
       }
     }
     // ---- writes
@@ -636,7 +645,7 @@ hipError_t vcap_beam_cand_dispatch(const BeamState& st, const float* logits, con
 
 hipError_t vcap_beam_select_dispatch(const BeamState& st, int B, int nb, int L, int V, int chunks, int cur, int eos,
                                      float length_penalty, int S0, int anc_ld, hipStream_t s) {
-  if (B > 8 || nb > 8 || 2 * nb > kMaxK || L > 64 || anc_ld > 128 || nb * chunks * 2 * nb > 20 * 64)
+  if (B > 8 || nb > 8 || 2 * nb > kMaxK || L > 64 || anc_ld > 128 || nb * chunks * 2 * nb > select_nc(nb) * 64)
     return hipErrorInvalidValue;
 #define VCAP_SEL(NB)                                                                                       \
   if (nb == NB) {                                                                                          \

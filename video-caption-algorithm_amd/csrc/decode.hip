@@ -540,18 +540,25 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Residual GEMV (PRO_DIRECT + EPI_RESID, <= 16 rows, one 16-column tile per workgroup) whose K range
-// needs more fragments than 4 waves hold: the f32 mlp c_proj (K = 3072: 48 slabs of 16 per wave
-// would be 96 16-byte fragments per lane).  8 waves (two per SIMD) of NSL slabs each, every load
-// issued up front as in vcap_rows_gemv_kernel, split-K partials summed through LDS in a fixed order
-// ((w0 + w1) + (w2 + w3)) + ((w4 + w5) + (w6 + w7)).
+// Residual GEMV (PRO_DIRECT + EPI_RESID, 16-row chunks over blockIdx.y, one 16-column tile per
+// workgroup) whose K range needs more fragments than 4 waves hold: the f32 mlp c_proj (K = 3072 of
+// GPT-2 small: 48 slabs of 16 per wave would be 96 16-byte fragments per lane; K = 4096 of
+// GPT-2-medium).  8 waves (two per SIMD) of NSL slabs each, every weight load issued up front as in
+// vcap_rows_gemv_kernel, split-K partials summed through LDS in a fixed order
+// ((w0 + w1) + (w2 + w3)) + ((w4 + w5) + (w6 + w7)).  Up to 24 slabs the A fragments are loaded at
+// once too; past that (NSL = 32: 128 weight + 128 A registers would not fit the 256 of a 2-wave
+// SIMD) they come in batches of 8 slabs, two batches live, batch b + 2 issued once batch b's
+// MFMAs have consumed its registers (the activation rows are L2-resident: every workgroup reads them).
 template <typename T, int NSL>
 __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
   constexpr int E = Frag<T>::kElems, KS = 4 * E;
+  constexpr int AB = NSL <= 24 ? NSL : 8, NAB = NSL / AB;
+  static_assert(NSL % AB == 0, "A batches tile the wave's slabs");
   __shared__ __attribute__((aligned(16))) float red[8][256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int M = a.M, N = a.N;
+  const int m0 = blockIdx.y * 16;
   // a.half: two workgroups per 16-column tile, each streaming 8 columns' weights (as in
   // vcap_rows_gemv_kernel: lanes l and l ^ 8 load the same fragment), the stores of its 8 columns
   const bool half = a.half != 0;
@@ -560,32 +567,47 @@ __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
   const int wlane = half ? ((lane & 0x30) | (hsel << 3) | (lane & 7)) : lane;
   const int nslab = 8 * NSL, g0 = wave * NSL;
   const int ntiles = (N + 15) >> 4;
-  u32x4 af[NSL];
-  const long xo = (long)min(fr, M - 1) * a.ldx + fg * E;
+  u32x4 af[NAB > 1 ? 2 : 1][AB];
+  const long xo = (long)min(m0 + fr, M - 1) * a.ldx + fg * E;
+  auto aload = [&](int b) {
 #pragma unroll
-  for (int s = 0; s < NSL; ++s) af[s] = vcap_dec_aload(a.x, (xo + (g0 + s) * KS) * (long)sizeof(T));
+    for (int s = 0; s < AB; ++s)
+      af[b & 1][s] = vcap_dec_aload(a.x, (xo + (g0 + b * AB + s) * KS) * (long)sizeof(T));
+  };
+  aload(0);
   asm volatile("" ::: "memory");  // the activation loads issue before the weights
   u32x4 wf[NSL];
   const u32x4* wp = packed_frag(a.w, min(n0 / 16, ntiles - 1), nslab, g0, wlane);
 #pragma unroll
   for (int s = 0; s < NSL; ++s) wf[s] = vcap_dec_wload<true>(a.w, wp + s * 64);
+  if constexpr (NAB > 1) aload(1);
   const int row = (tid >> 4) & 15, col = tid & 15;
-  const int mc = min(row, M - 1), nc = min(n0 + col, N - 1);
+  const int mc = min(m0 + row, M - 1), nc = min(n0 + col, N - 1);
   const float bl = *(a.bias ? a.bias + nc : (const float*)a.x);
   const float pre_bias = a.bias ? bl : 0.f;
   const float pre_res = ((const float*)a.out)[(long)mc * a.ldo + nc];
-  asm volatile("" : "+v"(af[0])::"memory");
+  asm volatile("" : "+v"(af[0][0])::"memory");
   f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < NSL; ++s) acc = mfma_frag(af[s], wf[s], acc, (T*)nullptr);
+  for (int b = 0; b < NAB; ++b) {
+#pragma unroll
+    for (int s = 0; s < AB; ++s) acc = mfma_frag(af[b & 1][s], wf[b * AB + s], acc, (T*)nullptr);
+    if (b + 2 < NAB) {
+      // batch b consumed before its registers reload, and the batch's 8 loads issue together (the
+      // scheduler otherwise sinks each to its use: 8 serial L2 round trips)
+      __builtin_amdgcn_sched_barrier(0);
+      aload(b + 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wave][(fg * 4 + r) * 16 + fr] = acc[r];
   __syncthreads();
-  if (tid < 256 && row < M && n0 + col < N && (hsel < 0 || (col >> 3) == hsel)) {
+  if (tid < 256 && m0 + row < M && n0 + col < N && (hsel < 0 || (col >> 3) == hsel)) {
     const int e = tid;
     const float v = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) +
                     ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e])) + pre_bias;
-    ((float*)a.out)[(long)row * a.ldo + n0 + col] = pre_res + v;
+    ((float*)a.out)[(long)(m0 + row) * a.ldo + n0 + col] = pre_res + v;
   }
 }
 
@@ -1173,10 +1195,17 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
       try_gemv<T, MT, NTB, PRO, EPI, 12>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 16>(nsl, a, s, err) ||
       try_gemv<T, MT, NTB, PRO, EPI, 24>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 32>(nsl, a, s, err))
     return err;
-  if constexpr (sizeof(T) == 4 && MT == 1 && NTB == 1 && PRO == PRO_DIRECT && EPI == EPI_RESID) {
-    if (nsl == 48) {  // f32 mlp c_proj of GPT-2 small (K = 3072): 8 waves x 24 slabs
-      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 24>), dim3((a.half ? 2 : 1) * ((a.N + 15) / 16)), dim3(512),
-                         0, s, a);
+  if constexpr (sizeof(T) == 4 && NTB == 1 && PRO == PRO_DIRECT && EPI == EPI_RESID) {
+    // f32 mlp c_proj (K = 3072 GPT-2 small / 4096 GPT-2-medium): 8 waves x 24 / 32 slabs, 16-row
+    // chunks over blockIdx.y (r05: the beam searches' 24-32 rows had taken the 64-workgroup
+    // generic kernel, 21 us per launch at K = 4096)
+    const dim3 grid((a.half ? 2 : 1) * ((a.N + 15) / 16), (a.M + 15) / 16);
+    if (nsl == 48 && a.M <= 64) {
+      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 24>), grid, dim3(512), 0, s, a);
+      return hipGetLastError();
+    }
+    if (nsl == 64 && a.M <= 64) {
+      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 32>), grid, dim3(512), 0, s, a);
       return hipGetLastError();
     }
   }
@@ -1391,6 +1420,201 @@ hipError_t vcap_lm_head_screen_dispatch(const RowsGemmArgs& a, int* nblk_out, in
   return ok ? err : hipErrorNotSupported;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Beam-search lm_head (PRO_LN + EPI_LSE) at M <= 32 rows as a weight stream (r05): the structure of
+// vcap_lm_head_stream_kernel - one workgroup per CU over a contiguous range of `tpw` 16-column tiles,
+// ln_f once per workgroup, the next group's weight fragments in flight during this group's MFMAs -
+// with both 16-row halves of a 32-row beam step (8 sequences x 4 beams) in the workgroup, so each
+// weight byte is read once per step (the 64-column GEMV blocks take 16-row chunks, and the 32-row
+// f32 step read the 206 MB GPT-2-medium vocab twice: 109 us).  Raw logits go to logits_raw,
+// bit-identical to the GEMV path's (same K split over the 4 waves, MFMA order and reduction); each
+// workgroup leaves one (max, sum exp(x - max)) partial per row, kept online per thread and merged
+// over the 16 column lanes - the quantity of the GEMV epilogue's two-pass form (its rounding differs
+// at the ulp level), merged by vcap_beam_cand_kernel the same way over nblk = grid partials.
+template <typename T, int NSL, int NTB, int MT>
+__global__ __launch_bounds__(256) void vcap_lm_head_lse_kernel(RowsGemmArgs a, int tpw) {
+  extern __shared__ __attribute__((aligned(16))) char dyn[];  // A tile [MT * 16][K] T
+  constexpr int E8 = Frag<T>::kElems, KS = 4 * E8, K = 4 * NSL * KS;
+  constexpr int KC = (K + 255) / 256;
+  constexpr int RPW = MT * 4;  // ln_f rows per wave
+  __shared__ __attribute__((aligned(16))) float red[4][MT * NTB * 256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int M = a.M, N = a.N;
+  const int nslab = 4 * NSL, g0 = wave * NSL;
+  const int ntiles = (N + 15) >> 4;
+  const int t0 = blockIdx.x * tpw, t1 = min(t0 + tpw, ntiles);
+  const int ngr = (t1 - t0 + NTB - 1) / NTB;
+  auto issue = [&](u32x4 (&wf)[NSL][NTB], int gi) {
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) {
+      const u32x4* wp = packed_frag(a.w, min(t0 + gi * NTB + j, t1 - 1), nslab, g0, lane);
+#pragma unroll
+      for (int s = 0; s < NSL; ++s) wf[s][j] = vcap_dec_wload<true>(a.w, wp + s * 64);
+    }
+  };
+  // ln_f rows + the first group's weights, issued up front
+  u32x4 wA[NSL][NTB], wB[NSL][NTB];
+  f32x4 xv[RPW][KC], gv[KC], bv[KC];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const long xo = (long)min(wave + 4 * r, M - 1) * a.ldx;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      xv[r][c] = __builtin_bit_cast(f32x4, vcap_dec_aload(a.x, (xo + min(c * 256 + lane * 4, K - 4)) * 4L));
+  }
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    gv[c] = *reinterpret_cast<const f32x4*>(a.ln_g + min(c * 256 + lane * 4, K - 4));
+    bv[c] = *reinterpret_cast<const f32x4*>(a.ln_b + min(c * 256 + lane * 4, K - 4));
+  }
+  issue(wA, 0);
+  // ln_f (vcap_rows_gemv_kernel PRO_LN arithmetic; the clamped chunks past K do not contribute)
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int m = wave + 4 * r;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      if (c * 256 + lane * 4 < K) s += (xv[r][c].x + xv[r][c].y) + (xv[r][c].z + xv[r][c].w);
+    const float mean = wave_sum(s) / (float)K;
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      if (c * 256 + lane * 4 < K) {
+        const f32x4 d = xv[r][c] - mean;
+        ss += sumsq4(d);
+      }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)K + a.ln_eps);
+    const bool live = m < M;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      if (c * 256 + lane * 4 < K) {
+        const f32x4 y = live ? ln_affine4(xv[r][c], mean, rstd, gv[c], bv[c]) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        const int byte = (c * 256 + lane * 4) * (int)sizeof(T);
+        char* dst = dyn + (long)m * (K * (int)sizeof(T)) + ((((byte >> 4) ^ (m & 15))) << 4) + (byte & 15);
+        if constexpr (sizeof(T) == 2) {
+          *reinterpret_cast<u32x2*>(dst) = (u32x2){pack_bf2(y.x, y.y), pack_bf2(y.z, y.w)};
+        } else {
+          *reinterpret_cast<f32x4*>(dst) = y;
+        }
+      }
+    }
+  }
+  __syncthreads();  // A tile written
+  const int row = tid >> 4, col = tid & 15;
+  float rmx[MT], rsm[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    rmx[i] = -INFINITY;
+    rsm[i] = 0.f;
+  }
+  auto group = [&](const u32x4 (&wf)[NSL][NTB], int gi) {
+    f32x4 acc[MT][NTB];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+      const int chunk = (g0 + s) * 4 + fg;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int ar = i * 16 + fr;
+        const u32x4 A = *reinterpret_cast<const u32x4*>(dyn + (long)ar * K * sizeof(T) + ((chunk ^ fr) << 4));
+#pragma unroll
+        for (int j = 0; j < NTB; ++j) acc[i][j] = mfma_frag(A, wf[s][j], acc[i][j], (T*)nullptr);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTB; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wave][(i * NTB + j) * 256 + (fg * 4 + r) * 16 + fr] = acc[i][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int m = i * 16 + row;
+      if (m < M) {
+#pragma unroll
+        for (int j = 0; j < NTB; ++j) {
+          const int t = t0 + gi * NTB + j, n = t * 16 + col;
+          if (t < t1 && n < N) {
+            const int e = (i * NTB + j) * 256 + row * 16 + col;
+            const float v = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]) + 0.f;
+            a.logits_raw[(long)m * N + n] = v;
+            const float nm = fmaxf(rmx[i], v);
+            rsm[i] = rsm[i] * expf(rmx[i] - nm) + expf(v - nm);
+            rmx[i] = nm;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  };
+  for (int gi = 0; gi < ngr; gi += 2) {
+    if (gi + 1 < ngr) issue(wB, gi + 1);
+    group(wA, gi);
+    if (gi + 1 < ngr) {
+      if (gi + 2 < ngr) issue(wA, gi + 2);
+      group(wB, gi + 1);
+    }
+  }
+  // merge the 16 column lanes' partials of each row (a lane that saw no column holds (-inf, 0))
+  auto merge = [](float& m, float& s, float om, float os) {
+    const float nm = fmaxf(m, om);
+    s = s * (m == nm ? 1.f : expf(m - nm)) + os * (om == nm ? 1.f : expf(om - nm));
+    m = nm;
+  };
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    merge(rmx[i], rsm[i], dpp_f<DPP_XOR1>(rmx[i]), dpp_f<DPP_XOR1>(rsm[i]));
+    merge(rmx[i], rsm[i], dpp_f<DPP_XOR2>(rmx[i]), dpp_f<DPP_XOR2>(rsm[i]));
+    merge(rmx[i], rsm[i], dpp_f<DPP_HALF_MIRROR>(rmx[i]), dpp_f<DPP_HALF_MIRROR>(rsm[i]));
+    merge(rmx[i], rsm[i], dpp_f<DPP_MIRROR>(rmx[i]), dpp_f<DPP_MIRROR>(rsm[i]));
+    const int m = i * 16 + row;
+    if (col == 0 && m < M) {
+      a.part_val[(long)m * gridDim.x + blockIdx.x] = rmx[i];
+      a.part_sum[(long)m * gridDim.x + blockIdx.x] = rsm[i];
+    }
+  }
+}
+
+template <typename T, int NSL, int MT>
+static bool launch_lm_lse(const RowsGemmArgs& a, int* nblk_out, hipStream_t s, hipError_t& err) {
+  constexpr int NTB = (NSL <= 8) ? 4 : 2;  // two register sets of MT x NSL x NTB fragments
+  const int ntiles = (a.N + 15) / 16;
+  const int cus = vcap_device_cus();
+  const int tpw = (ntiles + cus - 1) / cus;
+  const int grid = (ntiles + tpw - 1) / tpw;
+  const size_t lds = (size_t)MT * 16 * (4 * NSL * 4 * Frag<T>::kElems) * sizeof(T);
+  static int limit = 0;
+  // more partials than the caller's buffers hold, or an LDS limit that cannot be raised: the
+  // 64-column GEMV blocks take the lm_head
+  if (grid > a.nblk || (size_t)allow_lds(vcap_lm_head_lse_kernel<T, NSL, NTB, MT>, limit) < lds) return false;
+  hipLaunchKernelGGL((vcap_lm_head_lse_kernel<T, NSL, NTB, MT>), dim3(grid), dim3(256), lds, s, a, tpw);
+  if (nblk_out) *nblk_out = grid;
+  err = hipGetLastError();
+  return true;
+}
+
+static bool try_lm_lse(int dt, const RowsGemmArgs& a, int* nblk_out, hipStream_t s, hipError_t& err) {
+  if (a.M > 32 || !a.logits_raw || !a.part_val || !a.part_sum) return false;
+  if ((long)a.M * a.ldx * 4 >= 0x7FFFFFFFL) return false;
+  const int nsl = a.K / (16 * (dt == VCAP_DT_BF16 ? 8 : 4));
+  const bool two = a.M > 16;
+#define VCAP_LSE(TT, NN)                                                                           \
+  if (nsl == NN) return two ? launch_lm_lse<TT, NN, 2>(a, nblk_out, s, err) : launch_lm_lse<TT, NN, 1>(a, nblk_out, s, err);
+  if (dt == VCAP_DT_BF16) {
+    VCAP_LSE(bf16_t, 6) VCAP_LSE(bf16_t, 8)
+  } else {
+    VCAP_LSE(float, 12) VCAP_LSE(float, 16)
+  }
+#undef VCAP_LSE
+  return false;
+}
+
 // 16-column tiles per workgroup: the lm_head always takes 4 (argmax partials per 64 columns; 786
 // workgroups at 2 per CU.  r03: 2, 5 or 8 tiles per workgroup (1571 / 629 / 393 workgroups) measured
 // +1-2 / +6 / +8 us per token step, and forcing 3 workgroups per CU (<= 168 VGPRs) +22 us);
@@ -1417,6 +1641,10 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
   if (pro == PRO_LN && epi == EPI_LOGITS) {
     hipError_t err = hipSuccess;
     if (try_lm_stream(dt, a, nblk_out, s, err)) return err;
+  }
+  if (pro == PRO_LN && epi == EPI_LSE) {
+    hipError_t err = hipSuccess;
+    if (try_lm_lse(dt, a, nblk_out, s, err)) return err;
   }
   const int ntb = rows_ntb(epi, a.N, a.max_blocks);
   if (nblk_out) *nblk_out = (a.N + ntb * 16 - 1) / (ntb * 16);

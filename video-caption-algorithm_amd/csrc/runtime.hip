@@ -536,6 +536,7 @@ int issue_beam(const vcap_gpt2_desc* d, const vcap_beam_params* bp, const float*
   const int E = d->n_embd, nb = bp->num_beams, L = bp->max_new_tokens, R = B * nb;
   const int S0 = d->prefix_len + nids;
   const DecBufs& w = bb.w;
+  int nblk = bb.nblk;  // log_softmax partials per row the lm_head leaves (<= bb.nblk)
   auto lm_head = [&](int S_new) -> int {
     RowsGemmArgs g;
     memset(&g, 0, sizeof(g));
@@ -543,7 +544,8 @@ int issue_beam(const vcap_gpt2_desc* d, const vcap_beam_params* bp, const float*
     g.ln_g = d->lnf_g; g.ln_b = d->lnf_b; g.ln_eps = d->ln_eps;
     g.w = d->lm_head; g.N = d->vocab; g.K = E;
     g.logits_raw = bb.logits; g.part_val = bb.part_max; g.part_sum = bb.part_sum; g.nblk = bb.nblk;
-    VCAP_TRY(vcap_rows_gemm_dispatch(d->dtype, PRO_LN, EPI_LSE, g, nullptr, s), "lm_head_lse");
+    nblk = bb.nblk;
+    VCAP_TRY(vcap_rows_gemm_dispatch(d->dtype, PRO_LN, EPI_LSE, g, &nblk, s), "lm_head_lse");
     return 0;
   };
   VCAP_TRY(vcap_decode_init_dispatch(w.pt, R, bb.maxp, w.finished, w.nbanned, s), "decode_init");
@@ -560,7 +562,7 @@ int issue_beam(const vcap_gpt2_desc* d, const vcap_beam_params* bp, const float*
       if (int rc = run_layers(d, w, bb.maxp, bb.page_elems, R, 1, pos, 0, s, bb.st.anc, bb.anc_ld)) return rc;
       if (int rc = lm_head(1)) return rc;
     }
-    VCAP_TRY(vcap_beam_cand_dispatch(bb.st, bb.logits, bb.part_max, bb.part_sum, bb.nblk, R, d->vocab, nb, L, cur,
+    VCAP_TRY(vcap_beam_cand_dispatch(bb.st, bb.logits, bb.part_max, bb.part_sum, nblk, R, d->vocab, nb, L, cur,
                                      bp->repetition_penalty, bp->no_repeat_ngram_size, bp->min_new_tokens,
                                      bp->eos_token_id, bb.chunks, s),
              "beam_cand");

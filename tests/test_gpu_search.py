@@ -98,3 +98,35 @@ def test_caption_model_surface(device):
     texts = m.decoder.generate(emb.unsqueeze(1), prompt="", max_new_tokens=24, num_beams=1, temperature=1.0,
                                no_repeat_ngram_size=3, repetition_penalty=1.1)
     assert len(texts) == meta["B"]
+
+
+@pytest.mark.parametrize("nb,mx", [(3, 24), (4, 40)])
+def test_beam_search_32_rows_fp32_matches_reference(device, nb, mx):
+    """The bench's decode group shape for GPT-2 small (8 sequences x 3 / 4 beams = 24 / 32 rows): the
+    beam lm_head streamed with both 16-row halves in one workgroup (vcap_lm_head_lse_kernel, MT = 2) and
+    the f32 mlp c_proj on the 8-wave GEMV in two 16-row chunks; 4 copies of the reference's 2 clips give
+    the reference's hypotheses for every copy."""
+    meta, g, ga, dec, pre = _prefix("b16_b2", device)
+    reps = 8 // pre.shape[0]
+    rows = search.beam_search_device(dec, pre.repeat(reps, 1, 1).contiguous(), meta["prompt_ids"], num_beams=nb,
+                                     max_new_tokens=mx, min_new_tokens=8, no_repeat_ngram_size=3,
+                                     repetition_penalty=1.1, eos=ga.eos_token_id)
+    exp = g[f"beam{nb}_ids"]
+    assert np.array_equal(np.array(rows, dtype=np.int32), np.concatenate([exp] * reps)), rows
+
+
+@pytest.mark.parametrize("nb,mx", [(3, 24), (4, 40)])
+def test_beam_search_bf16_rows_invariant(device, nb, mx):
+    """bf16 device beam search: each of 4 copies of 2 sequences (24 / 32 rows: the streamed beam lm_head
+    with two row halves per workgroup) finds exactly the hypotheses of the 2 sequences searched alone
+    (6 / 8 rows: one row half) - every row's logits and log_softmax partials are computed the same way
+    whatever the row count."""
+    meta, g, va, ga, sd, frames = case("b16_b2")
+    dec = HipGPT2Decoder(sd, ga, "bf16", device)
+    pre = torch.from_numpy(g["inputs_embeds"][:, :4].copy()).to(device)
+    kw = dict(num_beams=nb, max_new_tokens=mx, min_new_tokens=8, no_repeat_ngram_size=3, repetition_penalty=1.1,
+              eos=ga.eos_token_id)
+    alone = search.beam_search_device(dec, pre, meta["prompt_ids"], **kw)
+    reps = 8 // pre.shape[0]
+    many = search.beam_search_device(dec, pre.repeat(reps, 1, 1).contiguous(), meta["prompt_ids"], **kw)
+    assert many == alone * reps, (many, alone)

@@ -733,10 +733,10 @@ def main():
         def fc1_flops(rows):
             return 2.0 * rows * va.mlp * va.dim
 
-        # bf16 ViT-B/16 frames (192 < tokens <= 208): the QKV projection and the attention run as one
-        # kernel (vcap_vit_qkv_attention) and the "vit.attention" probe times it; otherwise the probe
-        # times the attention kernel alone
-        fused_attn = (args.precision in ("bf16", "fp8") and 192 < va.tokens <= 208
+        # bf16 ViT-B/16 and ViT-L/14 frames (192 < tokens <= 208, 256 < tokens <= 272): the QKV
+        # projection and the attention run as one kernel (vcap_vit_qkv_attention) and the
+        # "vit.attention" probe times it; otherwise the probe times the attention kernel alone
+        fused_attn = (args.precision in ("bf16", "fp8") and (192 < va.tokens <= 208 or 256 < va.tokens <= 272)
                       and not {"qkv", "proj"} & set(enc.mx_gemms))
 
         def attn_flops(rows):
@@ -813,7 +813,7 @@ def main():
                          "timing": "HIP events around each fc1 launch on its stream inside the timed region "
                                    "(vcap_probe_*), read right after it; priced per launch population",
                          "other_populations": fc1["other_populations"]},
-            "attention": {"kernel": ("vit.attention = vcap_vit_qkv_attention_kernel (QKV projection + attention)"
+            "attention": {"kernel": ("vit.attention = vcap_vit_qkv_attention kernel (QKV projection + attention)"
                                      if fused_attn else "vit.attention"),
                           "bound": "mfma" if fused_attn else "hbm", "avg_launch_ms": att["avg_launch_ms"],
                           "launch_rows": M, "launches": att["launches"],

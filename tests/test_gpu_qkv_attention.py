@@ -2,8 +2,8 @@
 to the unfused pair it replaces in the bf16 encoder - vcap_gemm (bias, bf16 out) into a qkv buffer, then
 vcap_vit_attention (timm Attention.qkv + the attention core, src/models/video_encoder.py:112-121) - for
 every token row and for the class-token-only form of the last block, over frame counts that do and do not
-take the XCD-aware workgroup order (frames % 8), token counts across the supported range and head counts
-other than ViT-B's 12."""
+take the XCD-aware workgroup order (frames % 8), token counts across both supported ranges (ViT-B/16's
+193-208 and ViT-L/14's 257-272: vcap_vit_qkv_attention_l_kernel) and head counts other than 12 / 16."""
 import numpy as np
 import pytest
 import torch
@@ -45,7 +45,8 @@ def _fused(xn, w, b, BT, NT, H, cls_only):
 
 
 @pytest.mark.parametrize("BT,NT,H", [(16, 197, 12), (5, 197, 12), (8, 208, 12), (3, 193, 12), (8, 200, 4),
-                                     (2, 197, 1)])
+                                     (2, 197, 1), (8, 257, 16), (3, 257, 16), (4, 272, 16), (2, 260, 4),
+                                     (16, 257, 16)])
 def test_fused_bit_identical(device, BT, NT, H):
     xn, w, b = _case(device, BT, NT, H, BT * 1000 + NT + H)
     ref = _unfused(xn, w, b, BT, NT, H)
@@ -76,6 +77,6 @@ def test_fused_vs_fp32_sdpa(device):
 def test_fused_refuses_other_shapes(device):
     xn, w, b = _case(device, 2, 197, 12, 1)
     lib = N.lib()
-    for nt in (192, 209, 257):
+    for nt in (192, 209, 256, 273):
         assert lib.vcap_vit_qkv_attention(xn.data_ptr(), w.data_ptr(), b.data_ptr(), xn.data_ptr(), 2, nt, 12, 0,
                                           _s()) == N.E_UNSUPPORTED

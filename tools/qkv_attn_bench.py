@@ -1,7 +1,8 @@
 """Fused QKV projection + attention (vcap_vit_qkv_attention) against the unfused pair (vcap_gemm with
 bias into a qkv buffer, then vcap_vit_attention) at the ViT-B/16 frame shape: bit-identity of the
 outputs (all rows, and the class-token-only form) and the median time per launch of each.
-Environment: BT (frames, default 256 = one 16-video encode), REPS."""
+Environment: BT (frames, default 256 = one 16-video encode), NT / H (tokens / heads: 197 / 12 = ViT-B/16,
+257 / 16 = ViT-L/14), REPS."""
 import os
 import statistics
 import sys
@@ -13,7 +14,7 @@ import torch  # noqa: E402
 
 from vcap import _native as N  # noqa: E402
 
-BT, NT, H = int(os.environ.get("BT", "256")), 197, 12
+BT, NT, H = int(os.environ.get("BT", "256")), int(os.environ.get("NT", "197")), int(os.environ.get("H", "12"))
 D = H * 64
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)

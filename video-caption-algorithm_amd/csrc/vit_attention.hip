@@ -652,13 +652,227 @@ __global__ __launch_bounds__(512) void vcap_vit_qkv_attention_kernel(const bf16_
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// The same fusion for the ViT-L/14 frame (257 tokens, 17 token tiles = 272 rows; configs[3]).  A
+// 64-wide K-tile of 272 token + 192 weight rows is 58 KiB, so three whole slots (174 KiB) do not fit;
+// the token rows keep three slots (102 KiB: they stream from the LayerNorm output once per head) and
+// the weight rows - L2-resident, shared by every frame of the head - two (48 KiB), 150 KiB in all.
+// The weight tile kt + 1 may only be written once both groups have read tile kt - 1 (its slot), i.e.
+// from group 0's read phase kt on, and group 1 reads it one barrier after group 0: so group 0 (the
+// leading group) stages every weight block, one K-tile ahead, and waits for them at the end of its MFMA
+// phase; the token blocks go two K-tiles ahead, 5 of 34 per K-tile from group 0 and 29 from group 1
+// (29 pieces per group: 8 / 7 / 7 / 7 per wave).  Arithmetic, K order, bias add and bf16 rounding are
+// those of vcap_vit_qkv_attention_kernel, so the output is bit-identical to the unfused QKV GEMM +
+// vcap_vit_attention_bf16_kernel<18, 17> pair.
+namespace qb {
+constexpr int TT = 17, FT = 12;                 // token tiles (272 tokens), feature tiles
+constexpr int RT = TT * 16, RW = FT * 16;       // 272 token rows, 192 weight rows
+constexpr int TSLOT = RT * 128, WSLOT = RW * 128;
+constexpr int NTS = 3, NWS = 2;
+constexpr int LDS = NTS * TSLOT + NWS * WSLOT;  // 153600 B
+constexpr int TBLK = RT / 8, WBLK = RW / 8;     // 34 token, 24 weight blocks (8 rows = 1 KiB) per K-tile
+constexpr int G0_TOK = TBLK - 29;               // token blocks of group 0 (29 .. 33)
+constexpr int NB_MAX = 8;                       // pieces per wave: 8 (waves 0, 4), 7 (others)
+}  // namespace qb
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in 0..8
+VCAP_DEV void qb_vm_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
+
+__global__ __launch_bounds__(512) void vcap_vit_qkv_attention_l_kernel(const bf16_t* __restrict__ xn,
+                                                                       const bf16_t* __restrict__ wqkv,
+                                                                       const float* __restrict__ bqkv,
+                                                                       bf16_t* __restrict__ out, int BT, int N, int H,
+                                                                       int cls_only) {
+  using namespace qb;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int D = H * 64;
+  const int b = blockIdx.x;
+  int bt, h;
+  if ((BT & 7) == 0) {
+    const int x = b & 7, j = b >> 3;
+    bt = (j / H) * 8 + x;
+    h = j - (j / H) * H;
+  } else {
+    bt = b / H;
+    h = b - bt * H;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int fgrp = wave & 3, tgrp = wave >> 2;
+  const int t0 = tgrp * 9, ntt = tgrp ? TT - 9 : 9;
+  char* const Tsl = smem;                     // token slots
+  char* const Wsl = smem + NTS * TSLOT;       // weight slots
+
+  // this wave's pieces: group-local block list 0..28, wave wig takes wig + 4 i; group 0's list is the
+  // 24 weight blocks then token blocks 29..33, group 1's the token blocks 0..28
+  const int wig = wave & 3;
+  const int npc = wig == 0 ? NB_MAX : NB_MAX - 1;
+  const int nw = tgrp == 0 ? WBLK / 4 : 0;  // weight pieces: group 0's list entries wig + 4 i < 24
+  const int nt = npc - nw;
+  const char* src[NB_MAX];
+  int dsto[NB_MAX];  // byte offset within the token / weight slot
+#pragma unroll
+  for (int i = 0; i < NB_MAX; ++i) {
+    const int li = min(wig + 4 * i, 28);
+    const bool wblk = tgrp == 0 && li < WBLK;
+    const int blk = wblk ? li : (tgrp == 0 ? (TBLK - G0_TOK) + (li - WBLK) : li);  // group 0: tokens 29..33
+    const int lr = blk * 8 + (lane >> 3);       // row within its region
+    const int c = (lane & 7) ^ (lr & 7);
+    const bf16_t* p;
+    if (!wblk) {
+      p = xn + ((long)bt * N + min(lr, N - 1)) * D;
+    } else {
+      const int f = lr;  // 0..191: q / k / v feature f & 63 of head h
+      p = wqkv + ((long)(f >> 6) * D + h * 64 + (f & 63)) * D;
+    }
+    src[i] = (const char*)(p + c * 8);
+    dsto[i] = blk * 1024;
+  }
+  auto stage_w = [&](int kt) {  // group 0: this wave's weight pieces of K-tile kt
+    char* dst = Wsl + (kt % NWS) * WSLOT;
+#pragma unroll
+    for (int i = 0; i < NB_MAX; ++i)
+      if (i < nw) glds16_attn(src[i] + kt * 128, dst + dsto[i]);
+  };
+  auto stage_t = [&](int kt) {  // this wave's token pieces of K-tile kt
+    char* dst = Tsl + (kt % NTS) * TSLOT;
+#pragma unroll
+    for (int i = 0; i < NB_MAX; ++i)
+      if (i >= nw && i < npc) glds16_attn(src[i] + kt * 128, dst + dsto[i]);
+  };
+
+  f32x4 acc[3][9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = D / 64;
+  stage_w(0);
+  stage_t(0);
+  if (nk > 1) stage_t(1);
+  qb_vm_wait(nk > 1 ? nt : 0);       // K-tile 0 landed (tile 1's token pieces may still fly)
+  qa_barrier();
+  if (tgrp == 1) qa_barrier();       // group 1 runs one barrier behind
+  for (int kt = 0; kt < nk; ++kt) {
+    // ---- read phase: fragments of K-tile kt; group 0 stages the weights of kt + 1 (the slot of
+    // kt - 1, read by both groups before the last barrier), every wave its token pieces of kt + 2
+    const char* Tb = Tsl + (kt % NTS) * TSLOT;
+    const char* Wb = Wsl + (kt % NWS) * WSLOT;
+    u32x4 wf[2][3], tf[2][9];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int row = (fgrp * 3 + i) * 16 + fr;
+        wf[s2][i] = *reinterpret_cast<const u32x4*>(Wb + row * 128 + (((s2 * 4 + fg) ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        if (j < ntt) {
+          const int row = (t0 + j) * 16 + fr;
+          tf[s2][j] = *reinterpret_cast<const u32x4*>(Tb + row * 128 + (((s2 * 4 + fg) ^ (row & 7)) << 4));
+        }
+      }
+    }
+    const int w_now = kt + 1 < nk ? nw : 0, t_now = kt + 2 < nk ? nt : 0;
+    if (w_now) stage_w(kt + 1);
+    if (t_now) stage_t(kt + 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragments in registers before the barrier
+    qb_vm_wait(w_now + t_now);                          // all but this phase's pieces: tokens of kt + 1
+    qa_barrier();
+    // ---- MFMA phase
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 9; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+          if (j < ntt) acc[i][j] = mfma_frag(wf[s2][i], tf[s2][j], acc[i][j], (bf16_t*)nullptr);
+    __builtin_amdgcn_s_setprio(0);
+    if (w_now) qb_vm_wait(t_now);  // group 0: the weights of kt + 1 landed before group 1 reads them
+    qa_barrier();
+  }
+  if (tgrp == 0) qa_barrier();       // balance group 1's extra barrier
+  qa_barrier();                      // every wave's fragment reads done: the token slots become the images
+
+  char* Ks = smem;
+  char* Vs = smem + RT * 128;
+  char* Qs = smem + 2 * RT * 128;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int ft = fgrp * 3 + i, part = ft >> 2;        // 0 q, 1 k, 2 v
+    const int d0 = (ft & 3) * 16 + 4 * fg;
+    const f32x4 bias = *reinterpret_cast<const f32x4*>(bqkv + part * D + h * 64 + d0);
+    char* img = part == 0 ? Qs : (part == 1 ? Ks : Vs);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      if (j < ntt) {
+        const int tok = (t0 + j) * 16 + fr;
+        const f32x4 v = acc[i][j] + bias;
+        const u32x2 pk = (u32x2){pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
+        *reinterpret_cast<u32x2*>(img + tok * 128 + (((d0 >> 3) ^ (tok & 7)) << 4) + (d0 & 7) * 2) = pk;
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  qa_barrier();
+
+  constexpr int WAVES = 8, QT_MAX = 3;
+  const int qtiles = cls_only ? 1 : (N + 15) / 16;
+#pragma unroll
+  for (int i = 0; i < QT_MAX; ++i) {
+    const int qt = wave + i * WAVES;
+    if (qt >= qtiles) break;
+    u32x4 qf[2];
+    const int qrow = qt * 16 + fr;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      qf[s2] = *reinterpret_cast<const u32x4*>(Qs + qrow * 128 + (((s2 * 4 + fg) ^ (qrow & 7)) << 4));
+    f32x4 o[4];
+    float inv;
+    attn_bf16_qtile<18, 17>(Ks, Vs, qf, N, o, inv);
+    const int q = qt * 16 + fr;
+    const bool keep = q < N && (!cls_only || q == 0);
+    const long row = cls_only ? (long)bt : (long)bt * N + q;
+    attn_commit<false>(attn_pack<false>(o, inv, row, keep), out, D, h, nullptr, 0);
+  }
+}
+
 bool vcap_vit_qkv_attention_supported(int dt, int N, int H) {
-  return dt == VCAP_DT_BF16 && N > 12 * 16 && N <= 13 * 16 && H > 0 && H * 64 <= 4096;
+  return dt == VCAP_DT_BF16 && ((N > 12 * 16 && N <= 13 * 16) || (N > 16 * 16 && N <= 17 * 16)) && H > 0 &&
+         H * 64 <= 4096;
 }
 
 hipError_t vcap_vit_qkv_attention_dispatch(const void* xn, const void* wqkv, const float* bqkv, void* out, int BT,
                                            int N, int H, int cls_only, hipStream_t s) {
   if (!vcap_vit_qkv_attention_supported(VCAP_DT_BF16, N, H) || BT <= 0 || !bqkv) return hipErrorInvalidValue;
+  if (N > 13 * 16) {  // ViT-L/14: 17 token tiles
+    static bool configured_l = false;
+    if (!configured_l) {
+      hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_qkv_attention_l_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, qb::LDS);
+      if (e != hipSuccess) return e;
+      configured_l = true;
+    }
+    hipLaunchKernelGGL(vcap_vit_qkv_attention_l_kernel, dim3(BT * H), dim3(512), qb::LDS, s, (const bf16_t*)xn,
+                       (const bf16_t*)wqkv, bqkv, (bf16_t*)out, BT, N, H, cls_only);
+    return hipGetLastError();
+  }
   static bool configured = false;
   if (!configured) {
     hipError_t e = hipFuncSetAttribute((const void*)vcap_vit_qkv_attention_kernel,

@@ -154,7 +154,8 @@ int vcap_gemm(int in_dtype, int out_dtype, const void* A, int64_t lda, const voi
 int vcap_layernorm(int out_dtype, const float* x, int64_t ldx, void* y, int64_t ldy, const float* gamma,
                    const float* beta, int rows, int dim, float eps, void* stream);
 int vcap_vit_attention(int dtype, const void* qkv, void* out, int frames, int tokens, int heads, void* stream);
-/* Fused QKV projection + attention (bf16; 192 < tokens <= 208, i.e. ViT-B/16 frames): xn
+/* Fused QKV projection + attention (bf16; 192 < tokens <= 208 or 256 < tokens <= 272, i.e. ViT-B/16
+ * and ViT-L/14 frames): xn
  * [frames*tokens, heads*64] bf16 (the LayerNorm output), wqkv [3*heads*64, heads*64] bf16, bqkv
  * [3*heads*64] f32 -> out [frames*tokens, heads*64] bf16 (cls_only: [frames, heads*64], the class
  * token's row).  Bit-identical to vcap_gemm (bias, bf16 out) into a qkv buffer followed by

@@ -97,3 +97,17 @@ def test_l14_medium_bf16_close(device):
     assert np.abs(got - tv).max() < 1e-1
     sure = (tv[:, 0] - tv[:, 1]) > 0.1
     assert np.array_equal(ids[:, 0].cpu().numpy()[sure], g["hf_greedy_ids"][sure, 0])
+
+
+def test_medium_beam4_bf16_rows_invariant(device):
+    """bf16 GPT-2-medium beam 4 (configs[3]'s decoder): the reference clips searched alone (one 16-row half
+    per lm_head workgroup) and 4 copies of them at 32 rows (both halves in one workgroup,
+    vcap_lm_head_lse_kernel<bf16, 8, 4, 2>) give every copy the same hypotheses."""
+    meta, g, va, ga, enc, pre, dec, video = _models(device, "bf16")
+    prefix = torch.from_numpy(g["inputs_embeds"][:, :4].copy()).to(device)
+    kw = dict(num_beams=4, max_new_tokens=40, min_new_tokens=8, no_repeat_ngram_size=3, repetition_penalty=1.1,
+              eos=ga.eos_token_id)
+    alone = search.beam_search_device(dec, prefix, meta["prompt_ids"], **kw)
+    reps = 8 // prefix.shape[0]
+    many = search.beam_search_device(dec, prefix.repeat(reps, 1, 1).contiguous(), meta["prompt_ids"], **kw)
+    assert many == alone * reps, (many, alone)

@@ -1,0 +1,19 @@
+#!/bin/bash
+# configs[3] bf16 decode lanes after the beam-step rework and the L/14 fused kernel: 3 (auto) vs 2, ABAB,
+# quick legs off.
+out=${1:-gpurun_out/r5c3l}
+mkdir -p $out
+quick="--host-e2e 0 --cpu-baseline-s 0 --no-parity --no-decode-alone --strict-steps 0"
+C3="--vit vit_large_patch14_224 --gpt2 gpt2-medium --frames 32 --batch 4 --beams 4 --max-new 40 --steps 24 --warmup 4"
+for rep in 1 2; do
+  for l in 3 2; do
+    for P in bf16 fp32; do
+      tag="l${l}_${P}_$rep"
+      timeout -k 10 400 python -u bench.py $C3 $quick --dec-lanes $l --dec-precision $P > $out/$tag.json 2> $out/$tag.err || exit $?
+      python3 -c "
+import json
+d=json.loads(open('$out/$tag.json').read().strip().splitlines()[-1])
+print('$tag', round(d['value'],1), 'p50', round(d['p50_latency_ms'],1), {k: round(v,1) for k,v in d['stage_ms_p50'].items()})" | tee -a $out/summary.txt
+    done
+  done
+done

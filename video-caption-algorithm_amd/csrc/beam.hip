@@ -177,8 +177,9 @@ __global__ __launch_bounds__(256) void vcap_beam_cand_kernel(BeamState st, const
   }
 }
 
-// candidates per lane of the select kernel: a GPT-2 vocabulary's 25 chunks of top-2nb per beam
-// (NB = 4: 800 -> 13 per lane), at most 20
+// candidates per lane of the select kernel sized for a GPT-2 vocabulary's 25 chunks of top-2nb per
+// beam (NB = 4: 800 -> 13 per lane), at most 20; larger vocabularies take the 20-per-lane form
+constexpr int kSelNcMax = 20;
 constexpr int select_nc(int nb) {
   const int n = (nb * 25 * 2 * nb + 63) / 64;
   return n < 1 ? 1 : (n > 20 ? 20 : n);
@@ -198,11 +199,10 @@ VCAP_DEV int pick(const int (&a)[NB], int idx) {
 // One workgroup, wave b = batch b (B <= 8: 2 waves per SIMD, a 256-register budget).  Restates search.py beam_search (itself token-identical to the
 // reference's HF beam search, tests/test_gpu_search.py) for one step `cur`.  Lane p holds position
 // p (and p + 64 of the ancestry rows) of every beam of its batch; all state is loaded up front.
-template <int NB>
+template <int NB, int NC>   // NC: candidates per lane (NB * C * K <= 64 * NC)
 __global__ __launch_bounds__(512) void vcap_beam_select_kernel(BeamState st, int B, int L, int V, int C,
                                                                 int cur, int eos, float lpen, int S0, int anc_ld) {
   constexpr int K = 2 * NB;
-  constexpr int NC = select_nc(NB);   // candidates per lane (NB * C * K <= 64 * NC)
   __shared__ int s_unsat[8], s_allhits[8];
   const int lane = threadIdx.x & 63, b = threadIdx.x >> 6;
   const bool live = b < B;
@@ -645,13 +645,18 @@ hipError_t vcap_beam_cand_dispatch(const BeamState& st, const float* logits, con
 
 hipError_t vcap_beam_select_dispatch(const BeamState& st, int B, int nb, int L, int V, int chunks, int cur, int eos,
                                      float length_penalty, int S0, int anc_ld, hipStream_t s) {
-  if (B > 8 || nb > 8 || 2 * nb > kMaxK || L > 64 || anc_ld > 128 || nb * chunks * 2 * nb > select_nc(nb) * 64)
+  const int ncand = nb * chunks * 2 * nb;
+  if (B > 8 || nb > 8 || 2 * nb > kMaxK || L > 64 || anc_ld > 128 || ncand > kSelNcMax * 64)
     return hipErrorInvalidValue;
-#define VCAP_SEL(NB)                                                                                       \
-  if (nb == NB) {                                                                                          \
-    hipLaunchKernelGGL((vcap_beam_select_kernel<NB>), dim3(1), dim3(64 * B), 0, s, st, B, L, V, chunks, cur, \
-                       eos, length_penalty, S0, anc_ld);                                                   \
-    return hipGetLastError();                                                                              \
+#define VCAP_SEL(NB)                                                                                          \
+  if (nb == NB) {                                                                                             \
+    if (ncand <= select_nc(NB) * 64)                                                                          \
+      hipLaunchKernelGGL((vcap_beam_select_kernel<NB, select_nc(NB)>), dim3(1), dim3(64 * B), 0, s, st, B, L, V, \
+                         chunks, cur, eos, length_penalty, S0, anc_ld);                                       \
+    else                                                                                                      \
+      hipLaunchKernelGGL((vcap_beam_select_kernel<NB, kSelNcMax>), dim3(1), dim3(64 * B), 0, s, st, B, L, V,    \
+                         chunks, cur, eos, length_penalty, S0, anc_ld);                                       \
+    return hipGetLastError();                                                                                 \
   }
   VCAP_SEL(2) VCAP_SEL(3) VCAP_SEL(4) VCAP_SEL(5) VCAP_SEL(6) VCAP_SEL(7) VCAP_SEL(8)
 #undef VCAP_SEL

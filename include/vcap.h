@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 13
+#define VCAP_ABI_VERSION 14
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -281,6 +281,8 @@ typedef struct vcap_beam_params {
   int early_stopping;  /* only 0 (False) */
   int eos_token_id;
   int use_graph;
+  int max_blocks;      /* ABI v14: as vcap_gen_params.max_blocks - 0: whole-chip grids; > 0: cap each step's
+                          projection GEMV grids and the beam lm_head's grid near this many workgroups */
 } vcap_beam_params;
 size_t vcap_gpt2_beam_search_workspace_bytes(const vcap_gpt2_desc* d, int B, int num_beams, int S0,
                                              int max_new_tokens);

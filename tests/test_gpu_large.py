@@ -111,3 +111,15 @@ def test_medium_beam4_bf16_rows_invariant(device):
     reps = 8 // prefix.shape[0]
     many = search.beam_search_device(dec, prefix.repeat(reps, 1, 1).contiguous(), meta["prompt_ids"], **kw)
     assert many == alone * reps, (many, alone)
+
+
+def test_medium_beam4_fp32_32_rows_capped(device):
+    """The bench's configs[3] fp32 decode as the pipeline runs it: 32 rows with the step grids and the beam
+    lm_head capped at 96 workgroups (vcap_beam_params.max_blocks) - the reference's hypotheses per copy."""
+    meta, g, va, ga, enc, pre, dec, video = _models(device)
+    prefix = torch.from_numpy(g["inputs_embeds"][:, :4].copy()).to(device)
+    reps = 8 // prefix.shape[0]
+    rows = search.beam_search_device(dec, prefix.repeat(reps, 1, 1).contiguous(), meta["prompt_ids"], num_beams=4,
+                                     max_new_tokens=40, min_new_tokens=8, no_repeat_ngram_size=3,
+                                     repetition_penalty=1.1, eos=ga.eos_token_id, max_blocks=96)
+    assert np.array_equal(np.array(rows, dtype=np.int32), np.concatenate([g["beam4_ids"]] * reps)), rows

@@ -130,3 +130,20 @@ def test_beam_search_bf16_rows_invariant(device, nb, mx):
     reps = 8 // pre.shape[0]
     many = search.beam_search_device(dec, pre.repeat(reps, 1, 1).contiguous(), meta["prompt_ids"], **kw)
     assert many == alone * reps, (many, alone)
+
+
+@pytest.mark.parametrize("cap", [48, 96])
+def test_beam_search_capped_grids_fp32_matches_reference(device, cap):
+    """vcap_beam_params.max_blocks (ABI v14: the pipeline's decode grid cap, now applied to beam searches):
+    capped step GEMV grids (wider tiles, no half tiles) and a capped beam lm_head grid (more column tiles
+    per workgroup, fewer log_softmax partials) reproduce the reference's beam-3 / beam-4 ids at 8 and 32 rows."""
+    meta, g, ga, dec, pre = _prefix("b16_b2", device)
+    for nb, mx in ((3, 24), (4, 40)):
+        kw = dict(num_beams=nb, max_new_tokens=mx, min_new_tokens=8, no_repeat_ngram_size=3, repetition_penalty=1.1,
+                  eos=ga.eos_token_id, max_blocks=cap)
+        exp = g[f"beam{nb}_ids"]
+        rows = search.beam_search_device(dec, pre, meta["prompt_ids"], **kw)
+        assert np.array_equal(np.array(rows, dtype=np.int32), exp), (nb, rows, exp)
+        reps = 8 // pre.shape[0]
+        rows = search.beam_search_device(dec, pre.repeat(reps, 1, 1).contiguous(), meta["prompt_ids"], **kw)
+        assert np.array_equal(np.array(rows, dtype=np.int32), np.concatenate([exp] * reps)), (nb, rows)

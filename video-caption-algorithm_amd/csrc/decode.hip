@@ -1585,7 +1585,8 @@ template <typename T, int NSL, int MT>
 static bool launch_lm_lse(const RowsGemmArgs& a, int* nblk_out, hipStream_t s, hipError_t& err) {
   constexpr int NTB = (NSL <= 8) ? 4 : 2;  // two register sets of MT x NSL x NTB fragments
   const int ntiles = (a.N + 15) / 16;
-  const int cus = vcap_device_cus();
+  // one workgroup per CU, or per a.max_blocks (a beam search sharing the GPU with an encode)
+  const int cus = a.max_blocks > 0 ? std::min(vcap_device_cus(), a.max_blocks) : vcap_device_cus();
   const int tpw = (ntiles + cus - 1) / cus;
   const int grid = (ntiles + tpw - 1) / tpw;
   const size_t lds = (size_t)MT * 16 * (4 * NSL * 4 * Frag<T>::kElems) * sizeof(T);

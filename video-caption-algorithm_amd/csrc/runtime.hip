@@ -544,6 +544,7 @@ int issue_beam(const vcap_gpt2_desc* d, const vcap_beam_params* bp, const float*
     g.ln_g = d->lnf_g; g.ln_b = d->lnf_b; g.ln_eps = d->ln_eps;
     g.w = d->lm_head; g.N = d->vocab; g.K = E;
     g.logits_raw = bb.logits; g.part_val = bb.part_max; g.part_sum = bb.part_sum; g.nblk = bb.nblk;
+    g.max_blocks = bp->max_blocks;  // the streamed lm_head's grid (<= one workgroup per CU)
     nblk = bb.nblk;
     VCAP_TRY(vcap_rows_gemm_dispatch(d->dtype, PRO_LN, EPI_LSE, g, &nblk, s), "lm_head_lse");
     return 0;
@@ -559,7 +560,8 @@ int issue_beam(const vcap_gpt2_desc* d, const vcap_beam_params* bp, const float*
     if (cur > 0) {
       const int pos = S0 + cur - 1;
       VCAP_TRY(vcap_embed_tokens_dispatch(d->dtype, bb.st.tok_next, R, d->wte, d->wpe, w.h, E, pos, s), "embed");
-      if (int rc = run_layers(d, w, bb.maxp, bb.page_elems, R, 1, pos, 0, s, bb.st.anc, bb.anc_ld)) return rc;
+      if (int rc = run_layers(d, w, bb.maxp, bb.page_elems, R, 1, pos, bp->max_blocks, s, bb.st.anc, bb.anc_ld))
+        return rc;
       if (int rc = lm_head(1)) return rc;
     }
     VCAP_TRY(vcap_beam_cand_dispatch(bb.st, bb.logits, bb.part_max, bb.part_sum, nblk, R, d->vocab, nb, L, cur,
@@ -1230,6 +1232,7 @@ int vcap_gpt2_beam_search(const vcap_gpt2_desc* d, const vcap_beam_params* bp, c
                                     "prefix + prompt + max_new <= 128");
   if (B * nb * S0 > kMaxDecodeRows) return fail(VCAP_E_UNSUPPORTED, "B*num_beams*(prefix+prompt) exceeds max rows");
   if (bp->early_stopping != 0) return fail(VCAP_E_UNSUPPORTED, "only early_stopping=False (the reference's presets)");
+  if (bp->max_blocks < 0) return fail(VCAP_E_ARG, "vcap_gpt2_beam_search: max_blocks < 0");
   if (nb * vcap_beam_chunks(d->vocab) * 2 * nb > 20 * 64)
     return fail(VCAP_E_UNSUPPORTED, "num_beams too large for the vocabulary (candidate registers)");
   for (int i = 0; i < prompt_len; ++i)

@@ -16,7 +16,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
 DT_F32, DT_BF16, DT_MXFP8 = 0, 1, 2
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
@@ -70,7 +70,7 @@ class GenParams(C.Structure):
 class BeamParams(C.Structure):
     _fields_ = [("num_beams", i32), ("max_new_tokens", i32), ("min_new_tokens", i32),
                 ("no_repeat_ngram_size", i32), ("repetition_penalty", f32), ("length_penalty", f32),
-                ("early_stopping", i32), ("eos_token_id", i32), ("use_graph", i32)]
+                ("early_stopping", i32), ("eos_token_id", i32), ("use_graph", i32), ("max_blocks", i32)]
 
 
 class SampleParams(C.Structure):

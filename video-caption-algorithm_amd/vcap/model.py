@@ -396,7 +396,8 @@ class HipGPT2Decoder:
         bp = N.BeamParams(num_beams=int(cfg.num_beams), max_new_tokens=mx, min_new_tokens=int(cfg.min_new_tokens),
                           no_repeat_ngram_size=int(cfg.no_repeat_ngram_size),
                           repetition_penalty=float(cfg.repetition_penalty), length_penalty=float(cfg.length_penalty),
-                          early_stopping=0, eos_token_id=int(cfg.eos_token_id), use_graph=int(bool(cfg.use_graph)))
+                          early_stopping=0, eos_token_id=int(cfg.eos_token_id), use_graph=int(bool(cfg.use_graph)),
+                          max_blocks=int(cfg.max_blocks))
         arr = (C.c_int * max(len(ids), 1))(*ids)
         N.check(N.lib().vcap_gpt2_beam_search(C.byref(self.desc), C.byref(bp), prefix.data_ptr(), arr, len(ids), B,
                                               out.data_ptr(), lengths_out.data_ptr(), ws.data_ptr(), ws.numel(),

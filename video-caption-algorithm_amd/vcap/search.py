@@ -60,11 +60,13 @@ class _StepState:
 @torch.no_grad()
 def beam_search_device(dec, prefix: torch.Tensor, prompt_ids: Sequence[int], *, num_beams: int, max_new_tokens: int,
                        min_new_tokens: int = 8, no_repeat_ngram_size: int = 3, repetition_penalty: float = 1.1,
-                       eos: int = 50256, length_penalty: float = 1.0, use_graph: bool = True) -> List[List[int]]:
+                       eos: int = 50256, length_penalty: float = 1.0, use_graph: bool = True,
+                       max_blocks: int = 0) -> List[List[int]]:
     """The same search as `beam_search`, entirely on the device (vcap_gpt2_beam_search through
     HipGPT2Decoder.generate_ids: fused log_softmax / processor / top-2k kernels and a device
     bookkeeping kernel, one hipGraph, one device->host copy of the result).  Persistent
-    per-shape prefix / output buffers keep the captured graph across calls."""
+    per-shape prefix / output buffers keep the captured graph across calls.  max_blocks > 0 caps
+    the step's GEMV grids and the beam lm_head's grid (a search sharing the GPU with an encode)."""
     from .model import GenConfig
     B, P, E = prefix.shape
     cache = dec.__dict__.setdefault("_beam_bufs", {})   # persistent per decoder and shape
@@ -76,7 +78,7 @@ def beam_search_device(dec, prefix: torch.Tensor, prompt_ids: Sequence[int], *, 
     pre, out, lens = cache[key]
     pre.copy_(prefix)
     cfg = GenConfig(max_new_tokens, min_new_tokens, no_repeat_ngram_size, repetition_penalty, eos, eos, use_graph,
-                    num_beams=num_beams, length_penalty=length_penalty)
+                    num_beams=num_beams, length_penalty=length_penalty, max_blocks=max_blocks)
     dec.generate_ids(pre, prompt_ids, cfg, out=out, lengths_out=lens)
     ids = out.cpu()
     n = int(lens.max().item())

@@ -96,6 +96,12 @@ def parse():
                     help="skip the fp32 agreement check of the last timed batch")
     ap.add_argument("--no-decode-alone", dest="decode_alone", action="store_false",
                     help="skip the decode-step-alone measurement")
+    ap.add_argument("--token-exact-steps", type=int, default=-1,
+                    help="batches timed in the token_exact leg (the same pipeline with the reference's precision "
+                         "split: ViT bf16, GPT-2 decoder fp32) next to a bf16 headline; -1 = --steps, 0 disables")
+    ap.add_argument("--roctx", action="store_true",
+                    help="roctx stage ranges (ViT_Encoder / GPT2_Decoder_Step around the pipeline's launches, "
+                         "vcap/trace.py) for rocprofv3 --marker-trace --kernel-rename; off by default")
     ap.add_argument("--strict-steps", type=int, default=40,
                     help="batches timed in the strict_batch leg (one batch of --batch videos per encode and per "
                          "decode, no coalescing; 0 disables)")
@@ -133,9 +139,30 @@ def _fail(msg: str) -> int:
     return 2
 
 
+_GPU_COUNT = []
+
+
 def _visible_gpus() -> int:
+    """GPUs this process may use (HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES
+    applied), counted WITHOUT initialising HIP: the parent of self-launched ranks must not touch
+    the GPU before it starts them (a process that initialised HIP and then execs / forks children
+    that use the GPU is refused on this pool).  torch.cuda.device_count() would fall back to
+    torch._C._cuda_getDeviceCount() - a HIP initialisation - whenever amdsmi cannot answer, so the
+    amdsmi count is taken directly and a failure refuses the launch instead of falling back."""
+    if _GPU_COUNT:
+        return _GPU_COUNT[0]
     import torch
-    return torch.cuda.device_count()
+    count = getattr(torch.cuda, "_device_count_amdsmi", None)
+    if not torch.version.hip or count is None:
+        raise RuntimeError("cannot count GPUs without initialising HIP (no ROCm amdsmi device count)")
+    n = int(count())
+    if n < 0:
+        raise RuntimeError("amdsmi could not count the GPUs; refusing to fall back to a HIP initialisation "
+                           "in the launcher (set WORLD_SIZE via torchrun, or fix amdsmi)")
+    if torch.cuda.is_initialized():
+        raise RuntimeError("HIP was initialised while counting GPUs")
+    _GPU_COUNT.append(n)
+    return n
 
 
 def _free_port() -> int:
@@ -151,6 +178,13 @@ def launch_check(args) -> int | None:
     n = args.gpus
     if n < 1:
         return _fail(f"--gpus must be >= 1 (got {n})")
+    try:
+        return _launch_check(args, n)
+    except RuntimeError as e:
+        return _fail(str(e))
+
+
+def _launch_check(args, n: int):
     rehearsal = os.environ.get(REHEARSAL_ENV, "nccl") == "gloo"
     if "WORLD_SIZE" in os.environ:
         world = int(os.environ["WORLD_SIZE"])
@@ -174,6 +208,9 @@ def spawn_ranks(n: int) -> int:
     variables torchrun sets), wait for all, and return the worst status: the first failing rank's
     (a rank that fails leaves the others waiting in a collective, so they are then terminated)."""
     import subprocess
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():
+        return _fail("HIP is initialised in the launcher; the ranks must be started before any GPU call")
     env = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(_free_port()), VCAP_BENCH_LAUNCHER="bench.py --gpus (child ranks)")
     cmd = [sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]]
@@ -421,10 +458,10 @@ def parity_report(sd, va, ga, video, pre, enc, dec, cfg, last, dev):
     return rep
 
 
-def time_schedule(enc, pre, dec, cfg, video, prompt, dev, world, steps, warmup, **sched):
+def time_schedule(enc, pre, dec, cfg, video, prompt, dev, world, steps, warmup, keep_last=False, **sched):
     """Time `steps` batches of `video` through a fresh CaptionPipeline with the given schedule,
     bracketed like the headline (synchronize + barrier on both sides, max over ranks): captions/s,
-    per-batch latency stats (encode start -> ids) and B / p50."""
+    per-batch latency stats (encode start -> ids) and B / p50 (+ the last batch's ids as "_last")."""
     import torch
     import torch.distributed as dist
     from vcap.pipeline import CaptionPipeline
@@ -453,12 +490,16 @@ def time_schedule(enc, pre, dec, cfg, video, prompt, dev, world, steps, warmup, 
         elapsed = float(el.item())
         lat = [s.elapsed_time(e) for s, e in zip(starts, ends)]
         stage = ([s.elapsed_time(m) for s, m in zip(starts, mids)], [m.elapsed_time(e) for m, e in zip(mids, ends)])
+        last = pipe.result(pipe.last_slot).cpu() if keep_last else None
     finally:
         pipe.close()
     p50 = statistics.median(lat)
-    return {"value": world * B * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
-            "p50_latency_ms": p50, "captions_per_s_b_over_p50": world * B / (p50 / 1e3),
-            "latency_ms_stats": describe(lat), "_per_batch_ms": (lat, *stage)}
+    out = {"value": world * B * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
+           "p50_latency_ms": p50, "captions_per_s_b_over_p50": world * B / (p50 / 1e3),
+           "latency_ms_stats": describe(lat), "_per_batch_ms": (lat, *stage)}
+    if keep_last:
+        out["_last"] = last
+    return out
 
 
 def export(args, out, B, lat, vit_ms, dec_ms, ids_all, dec_alone, sweep_rows, eos, mem_mb):
@@ -555,6 +596,9 @@ def main():
     video = torch.from_numpy(frames_np).to(dev)
 
     N.check(N.lib().vcap_set_gemm_policy(args.gemm_policy), "gemm policy")
+    if args.roctx:
+        from vcap import trace
+        trace.enable()
     mx_gemms = tuple(g for g in args.mx_gemms.split(",") if g)
     enc = HipViTEncoder(sd, va, args.precision, dev, mx_gemms=mx_gemms)
     pre = HipPrefix(sd, ga.n_embd, device=dev)
@@ -669,6 +713,30 @@ def main():
         strict["schedule"] = (f"one {B}-video encode + one {B}-row decode graph per batch, {args.dec_lanes} decode "
                               f"lanes, encode stream off {STRICT_RESERVE} CUs, no coalescing")
         strict.pop("_per_batch_ms")
+    # token_exact: the same pipeline with the reference's precision split - ViT bf16 (its half-precision
+    # autocast, src/models/video_encoder.py:261-264), GPT-2 decoder fp32 (text_decoder.py:131-144) -
+    # timed like `value`; its last batch is checked against the CPU oracle below (8 of 8 expected)
+    token_exact = None
+    te_steps = args.steps if args.token_exact_steps < 0 else args.token_exact_steps
+    if (te_steps > 0 and not args.serial and args.precision == "bf16" and args.dec_precision == "bf16"
+            and args.beams == 1 and args.decode == "hf_greedy"):
+        dec32 = HipGPT2Decoder(sd, ga, "fp32", dev, screen=args.lm_screen == "on")
+        token_exact = time_schedule(enc, pre, dec32, cfg, video, prompt, dev, world, te_steps, args.warmup,
+                                    keep_last=True, dec_lanes=args.dec_lanes, dec_group=args.dec_group,
+                                    enc_group=args.enc_group, reserve_cus=args.reserve_cus)
+        lat_t, vit_t, dec_t = token_exact.pop("_per_batch_ms")
+        token_exact["stage_ms_p50"] = {"vit_encode_prefix": statistics.median(vit_t),
+                                       "prefix_ready_to_ids": statistics.median(dec_t)}
+        token_exact["precision"] = "ViT bf16 + GPT-2 decoder fp32 (bf16 lm_head screen + exact f32 rescoring)" \
+            if dec32.screen else "ViT bf16 + GPT-2 decoder fp32"
+        token_exact["schedule"] = "the headline's (same lanes, groups, CU reservation and decode grid cap)"
+        if args.decode_alone:
+            with torch.cuda.stream(torch.cuda.Stream(dev)):
+                _, pre_a = enc.encode(video, pre)
+                step_s, _ = decode_step_alone(dec32, pre_a, cfg, ga)
+            token_exact["decode_step_alone_us"] = step_s * 1e6
+        del dec32
+        torch.cuda.empty_cache()
     sweep = None
     sweep_rows = {}   # batch size -> the default schedule's per-batch rows (reference export shape)
     if args.batch_sizes:
@@ -733,11 +801,10 @@ def main():
         def fc1_flops(rows):
             return 2.0 * rows * va.mlp * va.dim
 
-        # bf16 ViT-B/16 and ViT-L/14 frames (192 < tokens <= 208, 256 < tokens <= 272): the QKV
-        # projection and the attention run as one kernel (vcap_vit_qkv_attention) and the
-        # "vit.attention" probe times it; otherwise the probe times the attention kernel alone
-        fused_attn = (args.precision in ("bf16", "fp8") and (192 < va.tokens <= 208 or 256 < va.tokens <= 272)
-                      and not {"qkv", "proj"} & set(enc.mx_gemms))
+        # where the encode runs the QKV projection and the attention as one kernel
+        # (vcap_vit_qkv_attention: bf16 ViT-B/16 and ViT-L/14 frames) the "vit.attention" probe times
+        # it; otherwise the probe times the attention kernel alone
+        fused_attn = enc.fuses_qkv_attention(0)   # the library's own predicate (every probed block alike)
 
         def attn_flops(rows):
             core = 4.0 * (rows // va.tokens) * va.heads * va.tokens * va.tokens * 64
@@ -830,6 +897,7 @@ def main():
                               "frac": t_roof / (elapsed / args.steps),
                               "vit_tflop": vit_exec / 1e12, "decode_weight_gb": dec_bytes / 1e9},
             "strict_batch": strict,
+            "token_exact": None,
             "batch_sweep": sweep,
             "pmc": pmc_summary(args.vit, args.gpt2, M, args.precision),
             "parity": parity,
@@ -855,8 +923,13 @@ def main():
                 out["oracle_parity"] = oracle_agreement(last, ref_ids, ga.eos_token_id)
                 if args.precision == "fp32":
                     out["parity"] = out["oracle_parity"]
+                if token_exact is not None:
+                    token_exact["oracle_parity"] = oracle_agreement(token_exact["_last"], ref_ids, ga.eos_token_id)
         else:
             out["cpu_baseline"] = None
+        if token_exact is not None:
+            token_exact.pop("_last", None)
+            out["token_exact"] = token_exact
         if args.export_csv or args.export_json:
             export(args, out, B, lat, vit_ms, dec_ms, ids_all, dec_alone, sweep_rows, ga.eos_token_id,
                    torch.cuda.max_memory_allocated(dev) / 2**20)

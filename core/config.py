@@ -2,7 +2,9 @@
 
 Differences, all additive: `backend` defaults to "hip" (the MI355X runtime; the reference's
 "torch" eager backend is not shipped - there is no CPU fallback), `precision` selects the
-operand dtype of the HIP kernels ("bf16" throughput mode, "fp32" parity mode), and
+operand dtype of the ViT kernels ("bf16" = the reference's half-precision autocast, "fp32" parity
+mode, "fp8" MXFP8 block GEMMs), `decoder_precision` the GPT-2 decoder's ("auto" = fp32 as in the
+reference, so the default surface is token-exact; "bf16" the throughput mode), and
 `prompt_ids*` let a caller pass pre-tokenised prompts when no GPT-2 BPE vocab is available.
 """
 from __future__ import annotations
@@ -69,7 +71,8 @@ class InferenceConfig:
     use_cupy_prefix_projector: bool = False
     cupy_prefix_force_fp16: bool = True
     # additive fields
-    precision: str = "bf16"
+    precision: str = "bf16"                 # ViT operands: bf16 (the reference's autocast) | fp32 | fp8
+    decoder_precision: str = "auto"         # GPT-2: auto = fp32, the reference's decoder (text_decoder.py:131-144)
     weights_seed: Optional[int] = None      # synthetic random-init weights when no ckpt is given
     tokenizer_dir: str = ""                 # local vocab.json + merges.txt for string prompts
     use_hipgraph: bool = True

@@ -28,6 +28,8 @@ def load_hip_caption_model(config: InferenceConfig):
     from vcap.caption import HipVideoCaptionModel, build_state_dict
     sd = build_state_dict(config.ckpt, config.vit_name, config.gpt2_name, config.weights_seed, config.prefix_len)
     model = HipVideoCaptionModel(sd, config.vit_name, config.gpt2_name, config.prefix_len, config.precision,
-                                 config.device, config.tokenizer_dir, config.use_hipgraph)
-    log.info("loaded %s + %s (%s) on %s", config.vit_name, config.gpt2_name, config.precision, config.device)
+                                 config.device, config.tokenizer_dir, config.use_hipgraph,
+                                 decoder_precision=config.decoder_precision)
+    log.info("loaded %s (%s) + %s (%s decoder) on %s", config.vit_name, config.precision, config.gpt2_name,
+             model.decoder_precision, config.device)
     return model

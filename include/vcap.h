@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VCAP_ABI_VERSION 14
+#define VCAP_ABI_VERSION 15
 
 /* VCAP_DT_MXFP8: OCP e4m3fn elements + one E8M0 scale per 32 consecutive K elements of a row
  * (the gfx950 block-scaled MFMA format; BASELINE configs[4]).  Scale arrays use the GEMM's
@@ -108,8 +108,10 @@ typedef struct vcap_gpt2_desc {
   const float* lnf_g; const float* lnf_b;
   const vcap_gpt2_layer* layers; /* host array of n_layer entries */
   /* f32 decoders, optional (NULL / 0 disable): a bf16 rows-packed copy of the lm_head and
-   * screen_bound = c * max_v ||w_v||_2 (c = 0.0043 covers the bf16 rounding of h and w and both
-   * f32 dot products over n_embd <= 1024).  A greedy step without requested logits then runs the
+   * screen_bound = c * max_v ||w_v||_2 with c >= 2u + u^2 + 4 * 1024 * 2^-24 = 8.07e-3 (u = 2^-8, the
+   * bf16 unit roundoff of EACH of h and w; the two f32 dot products over n_embd <= 1024, doubled
+   * for a truncating accumulator; vcap/model.py uses c = 0.0082).  The runtime scales the bound by
+   * max(rep, 1/rep) while a repetition penalty is active.  A greedy step without requested logits then runs the
    * lm_head in bf16 as a screen and rescores, in f32 against wte, every token whose exact score
    * could reach the screen's maximum: the token is the exact f32 argmax (processors applied, ties
    * to the lowest id) at half the lm_head's weight bytes. */
@@ -226,6 +228,11 @@ int vcap_rows_pack(int dtype, const void* w, int64_t ldw, int N, int K, void* pa
 size_t vcap_vit_workspace_bytes(const vcap_vit_desc* d, int B, int T);
 int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const float* frames, int B, int T,
                     float* enc_out, float* prefix_out, void* workspace, size_t ws_bytes, void* stream);
+/* ABI v15: 1 when vcap_vit_encode runs block `layer`'s QKV projection and attention as the fused
+ * vcap_vit_qkv_attention kernel, 0 when as a QKV GEMM + attention kernel (fp32 operands, MXFP8 QKV /
+ * attn-proj, other token counts), < 0 on a bad descriptor / layer.  The same predicate the encode
+ * uses, for callers that attribute FLOPs and bytes per kernel (bench.py). */
+int vcap_vit_layer_fuses_qkv_attention(const vcap_vit_desc* d, int layer);
 
 size_t vcap_gpt2_workspace_bytes(const vcap_gpt2_desc* d, int B, int S0, int max_new_tokens);
 int vcap_gpt2_generate(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* prompt_ids,

@@ -49,7 +49,11 @@ def parse(argv=None):
     ap.add_argument("--vit_name", default="vit_base_patch16_224")
     ap.add_argument("--gpt2_name", default="gpt2")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp8"],
-                    help="fp8 = MXFP8 ViT GEMMs (decoder bf16); fp32 = the parity mode")
+                    help="ViT arithmetic: bf16 = the reference's half-precision autocast; fp32 = the parity mode; "
+                         "fp8 = MXFP8 ViT GEMMs")
+    ap.add_argument("--decoder_precision", default="auto", choices=["auto", "fp32", "bf16"],
+                    help="GPT-2 decoder arithmetic: auto = fp32, the reference's (token-exact captions); "
+                         "bf16 = the throughput mode")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--preset", default="", help="decode a single candidate with this preset (precise/detailed/"
                                                  "natural/safe_sample); default runs the 3-candidate infer()")
@@ -70,7 +74,8 @@ def main(argv=None):
     args = parse(argv)
     frames = _frames_dir(args)
     cfg = InferenceConfig(ckpt=args.ckpt, vit_name=args.vit_name, gpt2_name=args.gpt2_name,
-                          num_frames=args.num_frames, precision=args.precision, device=args.device,
+                          num_frames=args.num_frames, precision=args.precision,
+                          decoder_precision=args.decoder_precision, device=args.device,
                           preset1=args.preset1, preset2=args.preset2, preset3=args.preset3, prompt1=args.prompt1,
                           prompt2=args.prompt2, prompt3=args.prompt3, tokenizer_dir=args.tokenizer_dir,
                           weights_seed=args.weights_seed)

@@ -57,3 +57,17 @@ def test_failing_rank_status_is_returned(tmp_path):
     r = _run(["--gpus", "2", "--dry-launch"], PYTHONPATH=str(tmp_path))
     assert r.returncode == 3, (r.stdout, r.stderr[-2000:])
     assert "dry_launch" not in r.stdout
+
+
+def test_gpu_count_never_falls_back_to_hip_init(tmp_path):
+    """When amdsmi cannot count the GPUs, the launcher refuses instead of calling
+    torch._C._cuda_getDeviceCount() (a HIP initialisation in the parent of the ranks): a sitecustomize
+    makes the amdsmi count fail and the HIP count exit with status 7 if it is ever reached."""
+    (tmp_path / "sitecustomize.py").write_text(
+        "import os, torch\n"
+        "torch.cuda._device_count_amdsmi = lambda: -1\n"
+        "def _hip_count():\n    os._exit(7)\n"
+        "torch._C._cuda_getDeviceCount = _hip_count\n")
+    r = _run(["--gpus", "2"], PYTHONPATH=str(tmp_path))
+    assert r.returncode == 2, (r.stdout, r.stderr[-2000:])
+    assert "amdsmi could not count" in r.stderr

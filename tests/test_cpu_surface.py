@@ -82,6 +82,20 @@ def test_cli_flags():
     from src.cli.inference import parse
     a = parse(["--video_path", "clip_dir", "--num_frames", "16", "--checkpoint", "x.pt"])
     assert a.video_path == "clip_dir" and a.num_frames == 16 and a.ckpt == "x.pt"
+    assert (a.precision, a.decoder_precision) == ("bf16", "auto")
+    assert parse(["--video_path", "d", "--decoder_precision", "bf16"]).decoder_precision == "bf16"
+
+
+def test_default_precision_split_is_the_references():
+    """The drop-in default decodes in fp32 (the reference's decoder, text_decoder.py:131-144) beside a
+    bf16 ViT (its half-precision autocast, video_encoder.py:261-264); bf16 decoding is opt-in."""
+    from vcap.caption import resolve_decoder_precision
+    c = InferenceConfig()
+    assert (c.precision, c.decoder_precision) == ("bf16", "auto")
+    assert [resolve_decoder_precision(p) for p in ("bf16", "fp32", "fp8")] == ["fp32"] * 3
+    assert resolve_decoder_precision("bf16", "bf16") == "bf16"
+    with pytest.raises(ValueError):
+        resolve_decoder_precision("bf16", "fp16")
 
 
 @pytest.mark.parametrize("n,w", [(8, 1), (8, 2), (64, 8), (10, 4), (3, 8)])

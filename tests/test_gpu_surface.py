@@ -206,3 +206,34 @@ def test_checkpoint_roundtrip(device, tmp_path):
     m2 = load_caption_model(cfg)
     ids2 = m2.generate_ids(torch.from_numpy(frames).to(device), [ga.bos_token_id])
     assert torch.equal(ids2, ids)
+
+
+def test_default_config_decodes_in_fp32(device):
+    """InferenceEngine(InferenceConfig()) - the drop-in default - runs the reference's precision split:
+    ViT in bf16 (the reference's half-precision autocast, src/models/video_encoder.py:261-264) and the
+    GPT-2 decoder in fp32 (text_decoder.py:131-144), so its greedy captions are those of an fp32
+    decoder (here: the full f32 lm_head on the same prefix) and, on the b16_b2 golden clips, the
+    reference's own greedy ids."""
+    from core.config import InferenceConfig
+    from core.engine import InferenceEngine
+    from vcap.model import GenConfig, HipGPT2Decoder
+    meta, g, va, ga, sd, frames = case("b16_b2")
+    cfg = InferenceConfig(device=str(device), num_frames=meta["T"], weights_seed=meta["weights_seed"])
+    assert (cfg.precision, cfg.decoder_precision) == ("bf16", "auto")
+    eng = InferenceEngine(cfg)
+    assert eng.model.hip_encoder.precision == "bf16"
+    assert eng.model.decoder_precision == "fp32"
+    hip = eng.model.decoder.hip
+    assert hip.precision == "fp32" and hip.dt == N.DT_F32 and hip.screen
+    video = torch.from_numpy(frames).to(device)
+    prefix = eng._prefix(video)
+    bos = [ga.bos_token_id]
+    got = eng.model.decoder.generate_from_prefix(prefix, bos, **GREEDY, min_new_tokens=8)
+    full = HipGPT2Decoder(sd, ga, "fp32", device, screen=False)
+    gc = GenConfig(24, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, True)
+    assert got == trim_generated(full.generate_ids(prefix, bos, gc), ga.eos_token_id)
+    assert got == g["hf_greedy_ids"].tolist()
+    # bf16 is still selectable (the throughput mode of the bench line)
+    eng16 = InferenceEngine(InferenceConfig(device=str(device), num_frames=meta["T"],
+                                            weights_seed=meta["weights_seed"], decoder_precision="bf16"))
+    assert eng16.model.decoder.hip.precision == "bf16"

@@ -6,6 +6,7 @@
 // decode (~60 launches per token) can be captured once into a hipGraph and replayed.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -428,12 +429,23 @@ struct Evicted {
   ~Evicted() { graph_entries_destroy(v); }
 };
 
+// The descriptor's bytes up to its last field: vcap_gpt2_desc ends in a pointer + a float, so its
+// 4 bytes of tail padding (whatever a C caller's stack held) stay out of the key; the int / float
+// head is 8 x 4 bytes, so no interior padding precedes the pointers.
+static_assert(offsetof(vcap_gpt2_desc, wte) == 8 * sizeof(int), "vcap_gpt2_desc: interior padding");
+static_assert(sizeof(vcap_gpt2_layer) == 12 * sizeof(void*), "vcap_gpt2_layer: padding");
+static_assert(sizeof(vcap_gen_params) == 8 * sizeof(int) && sizeof(vcap_beam_params) == 10 * sizeof(int),
+              "vcap_gen_params / vcap_beam_params: padding");
+static void put_gpt2_desc(std::string& k, const vcap_gpt2_desc* d) {
+  k.append((const char*)d, offsetof(vcap_gpt2_desc, screen_bound) + sizeof(d->screen_bound));
+  for (int l = 0; l < d->n_layer; ++l) k.append((const char*)&d->layers[l], sizeof(vcap_gpt2_layer));
+}
+
 std::string graph_key(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* ids,
                       int nids, int B, const int* out_ids, const float* logits, const void* ws) {
   std::string k;
   auto put = [&](const void* p, size_t n) { k.append((const char*)p, n); };
-  put(d, sizeof(*d));
-  for (int l = 0; l < d->n_layer; ++l) put(&d->layers[l], sizeof(vcap_gpt2_layer));
+  put_gpt2_desc(k, d);
   put(gp, sizeof(*gp));
   put(&prefix, sizeof(prefix));
   put(ids, sizeof(int) * (size_t)nids);
@@ -772,7 +784,8 @@ int vcap_vit_qkv_attention(const void* xn, const void* wqkv, const float* bqkv, 
   if (!xn || !wqkv || !bqkv || !out || frames <= 0 || tokens <= 0 || heads <= 0)
     return fail(VCAP_E_ARG, "vcap_vit_qkv_attention: bad arguments");
   if (!vcap_vit_qkv_attention_supported(VCAP_DT_BF16, tokens, heads))
-    return fail(VCAP_E_UNSUPPORTED, "vcap_vit_qkv_attention: needs 192 < tokens <= 208 and heads*64 <= 4096");
+    return fail(VCAP_E_UNSUPPORTED, "vcap_vit_qkv_attention: needs 192 < tokens <= 208 (ViT-B/16) or 256 < tokens <= 272 (ViT-L/14) "
+                "and heads*64 <= 4096");
   VCAP_TRY(vcap_vit_qkv_attention_dispatch(xn, wqkv, bqkv, out, frames, tokens, heads, cls_only ? 1 : 0,
                                            (hipStream_t)stream),
            "vcap_vit_qkv_attention");
@@ -819,6 +832,20 @@ size_t vcap_vit_workspace_bytes(const vcap_vit_desc* d, int B, int T) {
   return c.off;
 }
 
+// block `ly` runs QKV + attention as one kernel: bf16 operands (neither QKV nor attn-proj in MXFP8) at a
+// token count the fused kernel takes
+static bool vit_layer_fused(const vcap_vit_desc* d, const vcap_vit_layer& ly) {
+  const bool mx = d->dtype == VCAP_DT_MXFP8;
+  const int g = d->image / d->patch;
+  return !(mx && ly.qkv_ws) && !(mx && ly.proj_ws) && vcap_vit_qkv_attention_supported(vit_adt(d->dtype), g * g + 1, d->heads);
+}
+
+int vcap_vit_layer_fuses_qkv_attention(const vcap_vit_desc* d, int layer) {
+  if (int rc = check_vit(d)) return rc;
+  if (layer < 0 || layer >= d->depth) return fail(VCAP_E_ARG, "vcap_vit_layer_fuses_qkv_attention: layer out of range");
+  return vit_layer_fused(d, d->layers[layer]) ? 1 : 0;
+}
+
 int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const float* frames, int B, int T,
                     float* enc_out, float* prefix_out, void* workspace, size_t ws_bytes, void* stream) {
   if (int rc = check_vit(d)) return rc;
@@ -858,7 +885,7 @@ int vcap_vit_encode(const vcap_vit_desc* d, const vcap_prefix_desc* pd, const fl
     else
       VCAP_TRY(vcap_layernorm_dispatch(adt, w.x, D, w.xn, D, ly.ln1_g, ly.ln1_b, M, D, d->ln_eps, s), "norm1");
     GemmEpi e1{ly.qkv_b, nullptr, 0, 0, 0, 0, 0, 0, 0, mq ? w.xn_s : nullptr, mq ? ly.qkv_ws : nullptr, nullptr};
-    if (!mq && !mp && vcap_vit_qkv_attention_supported(adt, N, d->heads)) {
+    if (vit_layer_fused(d, ly)) {
       // QKV projection + attention in one kernel: q / k / v stay on chip
       ProbeScope ps(probe_attn, s, M);
       VCAP_TRY(vcap_vit_qkv_attention_dispatch(w.xn, ly.qkv_w, ly.qkv_b, w.attn, BT, N, d->heads, last, s),
@@ -1245,8 +1272,7 @@ int vcap_gpt2_beam_search(const vcap_gpt2_desc* d, const vcap_beam_params* bp, c
   if (!bp->use_graph) return issue_beam(d, bp, prefix, prompt_ids, prompt_len, B, out_ids, out_len, bb, s);
   std::string key = "beam";
   auto put = [&](const void* p, size_t n) { key.append((const char*)p, n); };
-  put(d, sizeof(*d));
-  for (int l = 0; l < d->n_layer; ++l) put(&d->layers[l], sizeof(vcap_gpt2_layer));
+  put_gpt2_desc(key, d);
   put(bp, sizeof(*bp));
   put(&prefix, sizeof(prefix));
   put(prompt_ids, sizeof(int) * (size_t)prompt_len);

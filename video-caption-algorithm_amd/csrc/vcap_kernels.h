@@ -123,7 +123,7 @@ hipError_t vcap_layernorm_dispatch(int out_dt, const float* x, long ldx, void* y
 // cls_only: only the class-token query of each (frame, head), written to compact row `frame`
 hipError_t vcap_vit_attention_dispatch(int dt, const void* qkv, void* out, int BT, int N, int H, hipStream_t s,
                                        int cls_only = 0);
-// fused QKV projection + attention (bf16, 192 < N <= 208): xn [BT*N, H*64] LayerNorm output, wqkv
+// fused QKV projection + attention (bf16, 192 < N <= 208 or 256 < N <= 272): xn [BT*N, H*64] LayerNorm output, wqkv
 // [3*H*64, H*64], bqkv [3*H*64] -> out as vcap_vit_attention_dispatch's
 bool vcap_vit_qkv_attention_supported(int dt, int N, int H);
 hipError_t vcap_vit_qkv_attention_dispatch(const void* xn, const void* wqkv, const float* bqkv, void* out, int BT,

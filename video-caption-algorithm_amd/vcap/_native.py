@@ -16,7 +16,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libvcap_hip.so"
 _lib = None
 
 DT_F32, DT_BF16, DT_MXFP8 = 0, 1, 2
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 vp, i32, i64, f32, sz = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t
 fp = C.POINTER(C.c_float)
@@ -107,6 +107,7 @@ SIGNATURES = {
     "vcap_rows_pack": (i32, [i32, vp, i64, i32, i32, vp, vp]),
     "vcap_vit_workspace_bytes": (sz, [C.POINTER(VitDesc), i32, i32]),
     "vcap_vit_encode": (i32, [C.POINTER(VitDesc), C.POINTER(PrefixDesc), vp, i32, i32, vp, vp, vp, sz, vp]),
+    "vcap_vit_layer_fuses_qkv_attention": (i32, [C.POINTER(VitDesc), i32]),
     "vcap_gpt2_workspace_bytes": (sz, [C.POINTER(GPT2Desc), i32, i32, i32]),
     "vcap_gpt2_generate": (i32, [C.POINTER(GPT2Desc), C.POINTER(GenParams), vp, C.POINTER(C.c_int), i32, i32, vp,
                                  vp, vp, sz, vp]),

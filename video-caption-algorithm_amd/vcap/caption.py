@@ -183,18 +183,33 @@ class HipTextDecoder:
         return [t.strip() for t in self.tokenizer.batch_decode(rows, skip_special_tokens=True)]
 
 
+def resolve_decoder_precision(precision: str, decoder_precision: str = "auto") -> str:
+    """The GPT-2 decoder's arithmetic.  "auto" = fp32 whatever the ViT runs in: the reference's own
+    split - its ViT under half-precision autocast (src/models/video_encoder.py:261-264,
+    backend_config.py:46), its decoder always fp32 (src/models/text_decoder.py:131-144) - so the
+    drop-in surface decodes token-exactly by default.  "bf16" is the throughput mode (BASELINE
+    configs[1] line of bench.py)."""
+    if decoder_precision == "auto":
+        return "fp32"
+    if decoder_precision not in ("bf16", "fp32"):
+        raise ValueError(f"decoder_precision must be auto, bf16 or fp32, got {decoder_precision!r}")
+    return decoder_precision
+
+
 class HipVideoCaptionModel:
     def __init__(self, sd, vit_name: str = "vit_base_patch16_224", gpt2_name: str = "gpt2", prefix_len: int = 4,
-                 precision: str = "bf16", device="cuda", tokenizer_dir: str = "", use_graph: bool = True):
+                 precision: str = "bf16", device="cuda", tokenizer_dir: str = "", use_graph: bool = True,
+                 decoder_precision: str = "auto"):
+        """precision: the ViT's operand type (bf16 / fp32 / fp8 = MXFP8 block GEMMs); decoder_precision:
+        see resolve_decoder_precision (default fp32, the reference's decoder arithmetic)."""
         self.device = torch.device(device)
         self.vit_arch, self.gpt2_arch = configs.vit_arch(vit_name), configs.gpt2_arch(gpt2_name)
         self.hip_encoder = HipViTEncoder(sd, self.vit_arch, precision, self.device)
         self.encoder = _Encoder(self.hip_encoder)
         self.proj = _Identity()
-        # "fp8" is a ViT-only mode (MXFP8 block GEMMs); the decoder then runs in bf16
-        self.decoder = HipTextDecoder(sd, self.gpt2_arch, "bf16" if precision == "fp8" else precision, self.device,
-                                      prefix_len, tokenizer_dir,
-                                      use_graph)
+        self.decoder_precision = resolve_decoder_precision(precision, decoder_precision)
+        self.decoder = HipTextDecoder(sd, self.gpt2_arch, self.decoder_precision, self.device, prefix_len,
+                                      tokenizer_dir, use_graph)
         self._engine_prefix = HipPrefix(sd, self.gpt2_arch.n_embd, prefix_len, 0.6, 0.4, self.device)
 
     def encode_prefix(self, video: torch.Tensor, ln_scale: Optional[float], in_weight: Optional[float]):

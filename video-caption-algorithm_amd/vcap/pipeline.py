@@ -36,6 +36,7 @@ import ctypes as C
 import torch
 
 from . import _native as N
+from . import trace
 from .model import GenConfig, HipGPT2Decoder, HipPrefix, HipViTEncoder, _Workspace
 
 
@@ -201,7 +202,10 @@ class CaptionPipeline:
     def _encode(self, video: torch.Tensor, slot: int, j0: int, n: int) -> None:
         """Encode n staged batches (on the encode stream) into submission positions j0.. of slot."""
         B = self.batch
-        self.enc.encode(video[:n * B], self.pre, out_prefix=self.group_prefix[slot][j0 * B:(j0 + n) * B])
+        # (roctx, off unless trace.enable(): the fused encode also runs the Cross_Modal_Alignment
+        # kernels - final LN, proj, engine LN-scale, mapper - at its tail)
+        with trace.range(trace.VIT):
+            self.enc.encode(video[:n * B], self.pre, out_prefix=self.group_prefix[slot][j0 * B:(j0 + n) * B])
         for ev in self._pending_mid:
             ev.record()
         self._pending_mid = []
@@ -226,8 +230,9 @@ class CaptionPipeline:
         s_dec = self.s_decs[lane]
         with torch.cuda.stream(s_dec):
             s_dec.wait_event(self.enc_done[slot])
-            self.dec.generate_ids(self.group_prefix[slot], self.prompt_ids, self.cfg, out=self.group_ids[slot],
-                                  workspace=self.dec_ws[lane])
+            with trace.range(trace.DECODE):
+                self.dec.generate_ids(self.group_prefix[slot], self.prompt_ids, self.cfg, out=self.group_ids[slot],
+                                      workspace=self.dec_ws[lane])
             out = self.group_ids[slot]
             if self.gather is not None:
                 out = self.gather(out, g * G)

@@ -321,12 +321,19 @@ def cpu_baseline(sd, va, ga, frames_np, budget_s: float, max_new: int, beams: in
             "_ids": ids8}
 
 
-def oracle_agreement(last, ref_ids, eos):
-    """Captions of the last timed batch against the CPU oracle's on the same frames (HF generate
-    output length: trimmed where every row has finished)."""
-    from vcap.model import trim_generated
-    got = trim_generated(last, eos)
-    exp = ref_ids.tolist() if hasattr(ref_ids, "tolist") else ref_ids
+def oracle_agreement(last, ref_ids, eos, beams: int = 1):
+    """Captions of the last timed batch against the CPU oracle's on the same frames.  Greedy: HF
+    generate's output length (trimmed where every row has finished).  Beam search: each row's best
+    hypothesis up to and including its first EOS (the device search and HF pad differently after
+    it)."""
+    from vcap.model import raw_greedy_tokens, trim_generated
+    import torch
+    if beams > 1:
+        got = raw_greedy_tokens(last, eos)
+        exp = raw_greedy_tokens(torch.as_tensor(ref_ids), eos)
+    else:
+        got = trim_generated(last, eos)
+        exp = ref_ids.tolist() if hasattr(ref_ids, "tolist") else ref_ids
     same = sum(int(a == b) for a, b in zip(got, exp))
     return {"against": "CPU oracle (fp32 restatement pinned to the reference's goldens) on the same frames",
             "batch": "last timed batch", "captions": len(exp), "captions_identical": same,
@@ -919,12 +926,11 @@ def main():
             cb = cpu_baseline(sd, va, ga, frames_np, args.cpu_baseline_s, args.max_new, args.beams)
             ref_ids = cb.pop("_ids")
             out["cpu_baseline"] = cb
-            if args.beams == 1:
-                out["oracle_parity"] = oracle_agreement(last, ref_ids, ga.eos_token_id)
-                if args.precision == "fp32":
-                    out["parity"] = out["oracle_parity"]
-                if token_exact is not None:
-                    token_exact["oracle_parity"] = oracle_agreement(token_exact["_last"], ref_ids, ga.eos_token_id)
+            out["oracle_parity"] = oracle_agreement(last, ref_ids, ga.eos_token_id, args.beams)
+            if args.precision == "fp32" and args.dec_precision == "fp32":
+                out["parity"] = out["oracle_parity"]
+            if token_exact is not None:
+                token_exact["oracle_parity"] = oracle_agreement(token_exact["_last"], ref_ids, ga.eos_token_id)
         else:
             out["cpu_baseline"] = None
         if token_exact is not None:

@@ -12,7 +12,7 @@
 out=$1; runner=$2; shift 2
 mkdir -p $out
 case $runner in
-  bench)  cmd="python bench.py --cpu-baseline-s 0 --host-e2e 0 --no-parity --no-decode-alone" ;;
+  bench)  cmd="python bench.py --cpu-baseline-s 0 --host-e2e 0 --no-parity --no-decode-alone --strict-steps 0 --token-exact-steps 0" ;;
   gemm)   cmd="python tools/gemm_bench.py" ;;
   attn)   cmd="python tools/attn_bench.py" ;;
   decode) cmd="python tools/decode_step_time.py" ;;

@@ -23,14 +23,13 @@ __device__ unsigned int g_vcap_stamp_n;
 #define VCAP_RT() ({ asm volatile("" ::: "memory"); unsigned long long _t = __builtin_amdgcn_s_memrealtime(); asm volatile("" ::: "memory"); _t; })
 #endif
 __device__ __forceinline__ void vcap_stamp_rec(unsigned long long tag, unsigned long long t0, unsigned long long t1,
-                                               unsigned long long t2, unsigned long long t3, unsigned long long t4) {
+                                               unsigned long long t2, unsigned long long t3, unsigned long long t4,
+                                               unsigned long long t5 = 0) {
   const unsigned i = atomicAdd(&g_vcap_stamp_n, 1u);
   if (i < (1u << 18)) {
     unsigned long long* r = g_vcap_stamps + 8ull * i;
     r[0] = tag; r[1] = blockIdx.x | ((unsigned long long)gridDim.x << 20) | ((unsigned long long)blockIdx.y << 40);
-    r[2] = t0; r[3] = t1; r[4] = t2; r[5] = t3; r[6] = t4;
-    r[7] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
-           ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);  // HW_ID | XCC_ID
+    r[2] = t0; r[3] = t1; r[4] = t2; r[5] = t3; r[6] = t4; r[7] = t5;
   }
 }
 extern "C" __attribute__((visibility("default"))) int vcap_diag_stamps(void* host, int max_rec) {
@@ -57,29 +56,37 @@ def header(sfx: str) -> str:
 
 def patch_decode(s: str) -> str:
     s = s.replace('#include "vcap_kernels.h"\n', '#include "vcap_kernels.h"\n' + header(""), 1)
-    # GEMV kernel
+    # GEMV kernel: entry | activation landed (PRO_LN: LayerNorm tile written + barrier; PRO_DIRECT: the
+    # last A fragment's load waited for) | weight stream landed (the last weight fragment waited for:
+    # loads retire in issue order) | MFMAs retired (partials in LDS) | reduction barrier | epilogue issued
     k0 = s.index("__global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {")
-    k1 = s.index("// General rows kernel", k0)
+    k1 = s.index("// Residual GEMV (PRO_DIRECT + EPI_RESID", k0)
     body = s[k0:k1]
     body = body.replace("  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n",
                         "  const unsigned long long t0 = VCAP_RT();\n  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n", 1)
     body = body.replace("  if constexpr (PRO == PRO_LN || EPI == EPI_LOGITS) __syncthreads();\n",
-                        "  if constexpr (PRO == PRO_LN || EPI == EPI_LOGITS) __syncthreads();\n  const unsigned long long t1 = VCAP_RT();\n", 1)
+                        "  if constexpr (PRO == PRO_LN || EPI == EPI_LOGITS) __syncthreads();\n"
+                        "  if constexpr (PRO == PRO_DIRECT) asm volatile(\"\" :: \"v\"(af[MTA - 1][NSL - 1].x));\n"
+                        "  const unsigned long long t1 = VCAP_RT();\n"
+                        "  asm volatile(\"\" :: \"v\"(wf[NSL - 1][NTB - 1].x));\n"
+                        "  const unsigned long long tw = VCAP_RT();\n", 1)
     body = body.replace("  if constexpr (EPI == EPI_LOGITS) toks.template mark<NTB>(a, m0, n0, s_rep, s_ban);\n  __syncthreads();\n",
                         "  const unsigned long long t2 = VCAP_RT();\n  if constexpr (EPI == EPI_LOGITS) toks.template mark<NTB>(a, m0, n0, s_rep, s_ban);\n  __syncthreads();\n  const unsigned long long t3 = VCAP_RT();\n", 1)
-    body = body.replace("  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0);\n}",
-                        "  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0);\n"
-                        "  if (threadIdx.x == 0) vcap_stamp_rec((unsigned long long)((NSL << 12) | (EPI << 8) | (PRO << 4) | NTB) | ((unsigned long long)MT << 20), t0, t1, t2, t3, VCAP_RT());\n}", 1)
-    assert body.count("VCAP_RT()") == 5, body.count("VCAP_RT()")
+    body = body.replace("  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0, hsel);\n}",
+                        "  rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0, hsel);\n"
+                        "  if (threadIdx.x == 0) vcap_stamp_rec((unsigned long long)((NSL << 12) | (EPI << 8) | (PRO << 4) | NTB) | ((unsigned long long)MT << 20) | ((unsigned long long)(hsel >= 0) << 24), t0, t1, tw, t2, t3, VCAP_RT());\n}", 1)
+    assert body.count("VCAP_RT()") == 6, body.count("VCAP_RT()")
     s = s[:k0] + body + s[k1:]
-    # decode attention (c64)
+    # decode attention (c64): entry | every load landed | output stored (issued)
     a0 = s.index("void vcap_decode_attention_c64_kernel(")
-    a1 = s.index("hipError_t vcap_decode_attention_dispatch", a0)
+    a1 = s.index("__global__ __launch_bounds__(64) void vcap_decode_attention_c64f_kernel", a0)
     att = s[a0:a1]
-    att = att.replace("  __shared__ float s_p[4][64];\n", "  __shared__ float s_p[4][64];\n  const unsigned long long t0 = VCAP_RT();\n", 1)
-    att = att.replace("  if (kg == 0) {\n    const float inv = 1.0f / sum;",
-                      "  const unsigned long long t2 = VCAP_RT();\n  if (kg == 0) {\n    const float inv = 1.0f / sum;", 1)
-    att = att[:att.rindex("}")] + "  if (threadIdx.x == 0) vcap_stamp_rec(0xA000ull, t0, t0, t2, t2, VCAP_RT());\n}\n\n"
+    att = att.replace("  __shared__ float s_p[64];\n", "  __shared__ float s_p[64];\n  const unsigned long long t0 = VCAP_RT();\n", 1)
+    att = att.replace("  c64_issue(L, q, kc, vc, maxp, m, h, H, seq, ctx);\n",
+                      "  c64_issue(L, q, kc, vc, maxp, m, h, H, seq, ctx);\n  asm volatile(\"\" :: \"v\"(L.vv[7].x));\n"
+                      "  const unsigned long long t1 = VCAP_RT();\n", 1)
+    att = att[:att.rindex("}")] + "  if (threadIdx.x == 0) vcap_stamp_rec(0xA000ull, t0, t1, t1, t1, t1, VCAP_RT());\n}\n\n"
+    assert att.count("VCAP_RT()") == 3, att.count("VCAP_RT()")
     s = s[:a0] + att + s[a1:]
     return s
 
@@ -93,7 +100,7 @@ def patch_attention(s: str) -> str:
     b = b.replace("  const int fr = lane & 15, fg = lane >> 4;\n", "  const int fr = lane & 15, fg = lane >> 4;\n  const unsigned long long t0 = VCAP_RT();\n", 1)
     b = b.replace('  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n  __syncthreads();\n',
                   '  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n  __syncthreads();\n  const unsigned long long t1 = VCAP_RT();\n', 1)
-    b = b[:b.rindex("}")] + "  __syncthreads();\n  if (threadIdx.x == 0) vcap_stamp_rec_attn(0xB000ull | KT, t0, t1, VCAP_RT(), 0, 0);\n}\n\n"
+    b = b[:b.rindex("}")] + "  __syncthreads();\n  if (threadIdx.x == 0) vcap_stamp_rec_attn(0xB000ull | KT, t0, t1, VCAP_RT(), 0, 0, 0);\n}\n\n"
     assert b.count("VCAP_RT()") == 3
     return s[:k0] + b + s[k1:]
 

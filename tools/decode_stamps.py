@@ -3,8 +3,10 @@
 alone, then for every launch of the replay reports (median over its workgroups, thread 0 of wave 0):
   start  = first workgroup entry - previous launch's last epilogue issue (the dependent boundary as
            the CUs see it, plus the last stores draining)
-  act    = entry -> activation operand ready (A fragments / LayerNorm tile written, barrier passed)
-  mfma   = -> MFMAs retired (partials written; waits for the weight stream)
+  act    = entry -> activation operand landed (PRO_LN: LayerNorm tile written, barrier passed;
+           PRO_DIRECT: the last A fragment's load returned)
+  wgt    = -> weight stream landed (the wave's last weight fragment returned)
+  mfma   = -> MFMAs retired (split-K partials written to LDS)
   red    = -> split-K reduction barrier passed
   epi    = -> epilogue issued
   skew   = last workgroup entry - first workgroup entry
@@ -34,14 +36,15 @@ def role(tag):
         return "attention"
     epi, pro, nsl = (tag >> 8) & 0xF, (tag >> 4) & 0xF, (tag >> 12) & 0xFF
     name = {0: "c_attn(LN+QKV)", 2: "c_fc(LN+GELU)", 1: "c_proj(+res)", 3: "lm_head(LN+proc)"}.get(epi, f"epi{epi}")
-    return f"{name} nsl{nsl}"
+    return f"{name} nsl{nsl}" + (" half" if (tag >> 24) & 1 else "")
 
 
 def main():
     name = os.environ.get("GPT2", "gpt2")
     ga = configs.gpt2_arch(name)
     dev = torch.device("cuda:0")
-    dec = HipGPT2Decoder(weights.synthetic_gpt2(1, ga), ga, "bf16", dev)
+    prec = os.environ.get("PREC", "bf16")
+    dec = HipGPT2Decoder(weights.synthetic_gpt2(1, ga), ga, prec, dev)
     lib = N.lib()
     lib.vcap_diag_stamps.restype = C.c_int
     lib.vcap_diag_stamps.argtypes = [C.c_void_p, C.c_int]
@@ -50,6 +53,7 @@ def main():
     with torch.cuda.stream(s):
         pre = torch.randn(B, 4, ga.n_embd, device=dev) * 0.1
         cfg = GenConfig(24, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, True)
+        cfg.max_blocks = int(os.environ.get("CAP", "0"))
         for _ in range(3):
             dec.generate_ids(pre, [ga.bos_token_id], cfg)
         torch.cuda.synchronize()
@@ -64,7 +68,7 @@ def main():
     launches, cur = [], []
     for r in rec:
         key = (int(r[0]), int(r[1]) >> 20 & 0xFFFFF)
-        if cur and (key != cur[0][0] or r[2] > max(x[1][6] for x in cur) + 200):
+        if cur and (key != cur[0][0] or r[2] > max(x[1][7] for x in cur) + 200):
             launches.append(cur)
             cur = []
         cur.append((key, r))
@@ -76,28 +80,27 @@ def main():
     for L in launches:
         rs = np.array([r for _, r in L])
         t0 = rs[:, 2].min()
-        end = rs[:, 6].max()
+        end = rs[:, 7].max()
         key = role(L[0][0][0]) + f" grid{L[0][0][1]}"
         d = per[key]
         if prev_end is not None and 0 <= t0 - prev_end < 10000:
             d["start"].append((t0 - prev_end) / 100)
             tot["start"] += (t0 - prev_end) / 100
-        d["act"].append(np.median(rs[:, 3] - rs[:, 2]) / 100)
-        d["mfma"].append(np.median(rs[:, 4] - rs[:, 3]) / 100)
-        d["red"].append(np.median(rs[:, 5] - rs[:, 4]) / 100)
-        d["epi"].append(np.median(rs[:, 6] - rs[:, 5]) / 100)
+        for c, (i, j) in {"act": (2, 3), "wgt": (3, 4), "mfma": (4, 5), "red": (5, 6), "epi": (6, 7)}.items():
+            d[c].append(np.median(rs[:, j] - rs[:, i]) / 100)
+            tot[c] += np.median(rs[:, j] - rs[:, i]) / 100
         d["skew"].append((rs[:, 2].max() - t0) / 100)
         d["span"].append((end - t0) / 100)
         tot["span"] += (end - t0) / 100
         prev_end = end
-    print(f"{name} B={B}: {len(launches)} launches, {n} workgroup records")
-    cols = ["start", "act", "mfma", "red", "epi", "skew", "span"]
+    print(f"{name} {prec} B={B} cap={cfg.max_blocks}: {len(launches)} launches, {n} workgroup records")
+    cols = ["start", "act", "wgt", "mfma", "red", "epi", "skew", "span"]
     print(f"{'launches':>8} " + " ".join(f"{c:>6}" for c in cols) + "  role")
     for key, d in sorted(per.items(), key=lambda kv: -sum(kv[1]["span"])):
         print(f"{len(d['span']):8d} " + " ".join(f"{statistics.median(d[c]) if d[c] else 0:6.2f}" for c in cols)
               + f"  {key}")
-    print(f"# sum of spans {tot['span']:.0f} us, of starts {tot['start']:.0f} us over the replay "
-          f"({len(launches)} launches)")
+    print(f"# sum over the replay ({len(launches)} launches): spans {tot['span']:.0f} us, starts {tot['start']:.0f} us; "
+          "median workgroup phases " + ", ".join(f"{c} {tot[c]:.0f}" for c in ("act", "wgt", "mfma", "red", "epi")) + " us")
 
 
 if __name__ == "__main__":

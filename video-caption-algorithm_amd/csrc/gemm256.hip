@@ -107,32 +107,31 @@ VCAP_DEV void epilogue256(const f32x4 (&acc)[2][2][4][2], int m0, int n0, int wr
     // blocks (qm, i + h) of a column block are adjacent in the mx_scale_index layout (row bits
     // 4..7 are its fastest index): they are collected in a register and stored as one u64 per
     // (lane, qn) instead of 8 scattered byte stores.
+    // Stores (r06): both 32-column blocks of a row pair are quantised before the lane-group transpose,
+    // so each 16-byte store instruction writes 64 contiguous bytes of a row (4 lanes) instead of 32:
+    // the 32-byte row pieces of the earlier layout cost this launch 238 -> 166 us alone at 50432 rows
+    // (fc1 shape; the same bytes: tools/mx_epi_check.py; profiles/r06_mx_fc1_epilogue_ab.txt).
     uint64_t sc[2] = {0, 0};
+    f32x4 biasq[2][2];
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        biasq[qn][j] = *reinterpret_cast<const f32x4*>(epi.bias + min(n0 + wc * 64 + qn * 32 + j * 16 + fg * 4, N - 4));
 #pragma unroll
     for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
-      for (int qn = 0; qn < 2; ++qn) {
-        const int nb = n0 + wc * 64 + qn * 32;
-        f32x4 bias[2];
+      for (int i = 0; i < 4; i += 2) {
+        uint32_t x[2][4];   // [qn][h * 2 + j]
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int n = min(nb + j * 16 + fg * 4, N - 4);
-          bias[j] = *reinterpret_cast<const f32x4*>(epi.bias + n);
-        }
-        // rows i and i+1 (16 apart) at a time: after quantisation the 4 lanes of a row hold 4
-        // fp8 of each 16-column half; a 4x4 lane-group transpose gives every lane 16 contiguous
-        // bytes (group 0: row i cols 0-15, 1: row i cols 16-31, 2 / 3: row i+1), one dwordx4
-#pragma unroll
-        for (int i = 0; i < 4; i += 2) {
-          uint32_t x[4];
+        for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const int m = m0 + wr * 128 + qm * 64 + (i + h) * 16 + fr;
             f32x4 v[2];
             float amax = 0.f;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-              v[j] = gelu_tanh4(acc[qm][qn][i + h][j] + bias[j]);
+              v[j] = gelu_tanh4(acc[qm][qn][i + h][j] + biasq[qn][j]);
 #pragma unroll
               for (int e = 0; e < 4; ++e) amax = fmaxf(amax, fabsf(v[j][e]));
             }
@@ -140,16 +139,19 @@ VCAP_DEV void epilogue256(const f32x4 (&acc)[2][2][4][2], int m0, int n0, int wr
             const int sbyte = mx_scale_byte(amax);
             const float inv = mx_inv_scale(sbyte);
             const f32x4 q0 = v[0] * inv, q1 = v[1] * inv;
-            x[2 * h] = pack_fp8x4(q0.x, q0.y, q0.z, q0.w);
-            x[2 * h + 1] = pack_fp8x4(q1.x, q1.y, q1.z, q1.w);
-            (void)m;
+            x[qn][2 * h] = pack_fp8x4(q0.x, q0.y, q0.z, q0.w);
+            x[qn][2 * h + 1] = pack_fp8x4(q1.x, q1.y, q1.z, q1.w);
             sc[qn] |= (uint64_t)(uint32_t)sbyte << (8 * (qm * 4 + i + h));
           }
-          transpose4_groups(x);
-          const int ms = m0 + wr * 128 + qm * 64 + (i + (fg >> 1)) * 16 + fr;
-          if (ms < M && nb < N)
-            out_store(reinterpret_cast<u32x4*>((uint8_t*)C + (long)ms * ldc + nb + (fg & 1) * 16),
-                      (u32x4){x[0], x[1], x[2], x[3]});
+        const int nb0 = n0 + wc * 64;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint32_t y[4] = {x[0][2 * h], x[0][2 * h + 1], x[1][2 * h], x[1][2 * h + 1]};
+          transpose4_groups(y);
+          const int ms = m0 + wr * 128 + qm * 64 + (i + h) * 16 + fr;
+          if (ms < M && nb0 < N)
+            out_store(reinterpret_cast<u32x4*>((uint8_t*)C + (long)ms * ldc + nb0 + fg * 16),
+                      (u32x4){y[0], y[1], y[2], y[3]});
         }
       }
 #pragma unroll

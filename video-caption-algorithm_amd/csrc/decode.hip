@@ -963,7 +963,7 @@ __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
   __shared__ int s_tok, s_nb;
   __shared__ __attribute__((aligned(16))) float s_hf[SCREEN ? 1024 : 4];
   __shared__ float s_red[4];
-  __shared__ int s_cb[SCREEN ? 64 : 1], s_cv[SCREEN ? 1024 : 1], s_bn[SCREEN ? 256 : 1];
+  __shared__ int s_cb[SCREEN ? 64 : 1], s_cv[SCREEN ? 4096 : 1], s_bn[SCREEN ? 256 : 1];
   __shared__ int s_ncb, s_ncv;
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // every load of the first phase issued at once (clamped addresses, selects after): the history,
@@ -1029,56 +1029,75 @@ __global__ __launch_bounds__(256) void vcap_decode_finalize_kernel(
         if (tid + q * 256 < nblk && pv[q] >= thr) s_cb[min(atomicAdd(&s_ncb, 1), 63)] = tid + q * 256;
       __syncthreads();
       const int ncb = s_ncb;
-      // the surviving columns of the candidate blocks into s_cv, 1024 column positions per pass (a
-      // candidate block holds tpb * 16 <= 512 columns: one pass for up to 2-4 candidate blocks);
-      // past 64 candidate blocks every block is scanned
+      // the surviving columns of the candidate blocks into s_cv, 2048 column positions per pass (a
+      // candidate block holds tpb * 16 <= 512 columns); past 64 candidate blocks every block is
+      // scanned.  Survivors accumulate over the passes and are rescored once at the end (or whenever
+      // the next pass could overflow s_cv), so the scan's proc loads and the rescoring's wte-row loads
+      // are two memory round trips for the usual handful of survivors, not two per pass.
       const bool all_blocks = ncb > 64;
       const int nsb = all_blocks ? nblk : ncb, span = sc.tpb * 16;
-      for (int from = 0; from < nsb * span; from += 1024) {
-        if (tid == 0) s_ncv = 0;
-        __syncthreads();
-        const int lim = min(from + 1024, nsb * span);
-        int cv[4];
-        float cp[4];
+      constexpr int PASS = 2048, CAP = 2 * PASS, CW = 4;
+      auto rescore = [&](int ncv) {
+        // CW candidates per wave at once (their wte rows' loads issued together); each candidate's dot
+        // product is one fma chain over the row in order
+        for (int i0 = wave; i0 < ncv; i0 += 4 * CW) {
+          int vv[CW];
+          f32x4 w4[CW][4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {  // the four loads issued together
+          for (int c = 0; c < CW; ++c) {
+            vv[c] = s_cv[min(i0 + 4 * c, ncv - 1)];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)  // E <= 1024
+              w4[c][r] = *reinterpret_cast<const f32x4*>(sc.w32 + (long)vv[c] * E + min(lane * 4 + r * 256, E - 4));
+          }
+#pragma unroll
+          for (int c = 0; c < CW; ++c) {
+            float d = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if (lane * 4 + r * 256 >= E) break;
+              const f32x4 h4 = *reinterpret_cast<const f32x4*>(s_hf + lane * 4 + r * 256);
+              d = fmaf(w4[c][r].w, h4.w, fmaf(w4[c][r].z, h4.z, fmaf(w4[c][r].y, h4.y, fmaf(w4[c][r].x, h4.x, d))));
+            }
+            float p = wave_sum(d);
+            // RepetitionPenalty -> NoRepeatNGram -> MinNewTokens, the lm_head epilogue's order
+            if (sc.rep != 1.0f) {
+              bool rep_hit = false;
+              for (int t = 0; t < step; ++t) rep_hit |= s_h[t] == vv[c];
+              if (rep_hit) p = p < 0.f ? p * sc.rep : p / sc.rep;
+            }
+            bool ban_hit = false;
+            for (int t = 0; t < nbc; ++t) ban_hit |= s_bn[t] == vv[c];
+            if (ban_hit) p = -INFINITY;
+            if (vv[c] == eos && step < sc.min_new) p = -INFINITY;
+            if (i0 + 4 * c < ncv) argmax_take(ev, ei, p, vv[c]);
+          }
+        }
+      };
+      if (tid == 0) s_ncv = 0;
+      __syncthreads();
+      for (int from = 0; from < nsb * span; from += PASS) {
+        const int lim = min(from + PASS, nsb * span);
+        int cv[PASS / 256];
+        float cp[PASS / 256];
+#pragma unroll
+        for (int r = 0; r < PASS / 256; ++r) {  // the pass's loads issued together
           const int i = from + tid + r * 256;
           const int bl = i / span, off = i - bl * span;
           cv[r] = i < lim ? (all_blocks ? bl : s_cb[min(bl, 63)]) * span + off : vocab;
           cp[r] = sc.proc[prow + min(cv[r], vocab - 1)];
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < PASS / 256; ++r)
           if (cv[r] < vocab && cp[r] >= thr) s_cv[atomicAdd(&s_ncv, 1)] = cv[r];
         __syncthreads();
         const int ncv = s_ncv;
-        for (int i = wave; i < ncv; i += 4) {
-          const int vv = s_cv[i];
-          f32x4 w4[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r)  // E <= 1024: the row's loads issued together
-            w4[r] = *reinterpret_cast<const f32x4*>(sc.w32 + (long)vv * E + min(lane * 4 + r * 256, E - 4));
-          float d = 0.f;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (lane * 4 + r * 256 >= E) break;
-            const f32x4 h4 = *reinterpret_cast<const f32x4*>(s_hf + lane * 4 + r * 256);
-            d = fmaf(w4[r].w, h4.w, fmaf(w4[r].z, h4.z, fmaf(w4[r].y, h4.y, fmaf(w4[r].x, h4.x, d))));
-          }
-          float p = wave_sum(d);
-          // RepetitionPenalty -> NoRepeatNGram -> MinNewTokens, the lm_head epilogue's order
-          if (sc.rep != 1.0f) {
-            bool rep_hit = false;
-            for (int t = 0; t < step; ++t) rep_hit |= s_h[t] == vv;
-            if (rep_hit) p = p < 0.f ? p * sc.rep : p / sc.rep;
-          }
-          bool ban_hit = false;
-          for (int t = 0; t < nbc; ++t) ban_hit |= s_bn[t] == vv;
-          if (ban_hit) p = -INFINITY;
-          if (vv == eos && step < sc.min_new) p = -INFINITY;
-          argmax_take(ev, ei, p, vv);
+        if (ncv > CAP - PASS || from + PASS >= nsb * span) {  // the next pass could overflow, or the last
+          rescore(ncv);
+          __syncthreads();  // s_cv / s_ncv reused
+          if (tid == 0) s_ncv = 0;
+          __syncthreads();
         }
-        __syncthreads();  // s_cv / s_ncv reused by the next pass
       }
       __syncthreads();  // s_red reads done
       if (lane == 0) {

@@ -549,23 +549,28 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
 // once too; past that (NSL = 32: 128 weight + 128 A registers would not fit the 256 of a 2-wave
 // SIMD) they come in batches of 8 slabs, two batches live, batch b + 2 issued once batch b's
 // MFMAs have consumed its registers (the activation rows are L2-resident: every workgroup reads them).
-template <typename T, int NSL>
+template <typename T, int NSL, bool SPLIT>
 __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
   constexpr int E = Frag<T>::kElems, KS = 4 * E;
   constexpr int AB = NSL <= 24 ? NSL : 8, NAB = NSL / AB;
   static_assert(NSL % AB == 0, "A batches tile the wave's slabs");
   __shared__ __attribute__((aligned(16))) float red[8][256];
+  __shared__ int s_ticket;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int M = a.M, N = a.N;
   const int m0 = blockIdx.y * 16;
   // a.half: two workgroups per 16-column tile, each streaming 8 columns' weights (as in
-  // vcap_rows_gemv_kernel: lanes l and l ^ 8 load the same fragment), the stores of its 8 columns
-  const bool half = a.half != 0;
+  // vcap_rows_gemv_kernel: lanes l and l ^ 8 load the same fragment), the stores of its 8 columns.
+  // SPLIT: two workgroups per 16-column tile, each taking one half of K for all 16 columns, so each
+  // ingests half the activation rows (the f32 mlp c_proj's 196 KiB of activations per workgroup was
+  // twice its weight slice: profiles/r06_decode_stamps.txt); the pair meets below.
+  const bool half = !SPLIT && a.half != 0;
   const int hsel = half ? (int)(blockIdx.x & 1) : -1;
-  const int n0 = half ? (int)(blockIdx.x >> 1) * 16 : (int)blockIdx.x * 16;
+  const int ksel = SPLIT ? (int)(blockIdx.x & 1) : 0;
+  const int n0 = (half || SPLIT) ? (int)(blockIdx.x >> 1) * 16 : (int)blockIdx.x * 16;
   const int wlane = half ? ((lane & 0x30) | (hsel << 3) | (lane & 7)) : lane;
-  const int nslab = 8 * NSL, g0 = wave * NSL;
+  const int nslab = (SPLIT ? 16 : 8) * NSL, g0 = (SPLIT ? ksel * 8 * NSL : 0) + wave * NSL;
   const int ntiles = (N + 15) >> 4;
   u32x4 af[NAB > 1 ? 2 : 1][AB];
   const long xo = (long)min(m0 + fr, M - 1) * a.ldx + fg * E;
@@ -603,11 +608,39 @@ __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wave][(fg * 4 + r) * 16 + fr] = acc[r];
   __syncthreads();
-  if (tid < 256 && m0 + row < M && n0 + col < N && (hsel < 0 || (col >> 3) == hsel)) {
-    const int e = tid;
-    const float v = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) +
-                    ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e])) + pre_bias;
-    ((float*)a.out)[(long)(m0 + row) * a.ldo + n0 + col] = pre_res + v;
+  if constexpr (SPLIT) {
+    // The K-half partials of a tile meet through global memory, the MI355X guide's valid hand-off
+    // form (Guideline 16 R1): every partial store is sc1 (agent-scope relaxed atomic store: write-
+    // through) and every storing wave drains (vmcnt(0)) before the workgroup barrier; then one lane
+    // takes a ticket (agent-scope atomic add, zeroed per decode by vcap_decode_init).  The pair's
+    // second arriver loads the other half's partial with sc1 loads and stores the output; the first
+    // exits.  Neither waits for the other (no spin), and the sum is p(K half 0) + p(K half 1) whichever
+    // arrives first, so the result is deterministic.
+    const long pair = (long)blockIdx.y * (gridDim.x >> 1) + (blockIdx.x >> 1);
+    float part = 0.f;
+    if (tid < 256) {
+      const int e = tid;
+      part = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) + ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e]));
+      __hip_atomic_store(a.sk_part + (pair * 2 + ksel) * 256 + e, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (tid == 0) s_ticket = __hip_atomic_fetch_add(a.sk_cnt + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if ((s_ticket & 1) == 0) return;  // first of the pair (tickets advance by 2 per launch)
+    if (tid < 256 && m0 + row < M && n0 + col < N) {
+      const float other =
+          __hip_atomic_load(a.sk_part + (pair * 2 + (ksel ^ 1)) * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float v = (ksel == 0 ? part + other : other + part) + pre_bias;
+      ((float*)a.out)[(long)(m0 + row) * a.ldo + n0 + col] = pre_res + v;
+    }
+  } else {
+    if (tid < 256 && m0 + row < M && n0 + col < N && (hsel < 0 || (col >> 3) == hsel)) {
+      const int e = tid;
+      const float v = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) +
+                      ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e])) + pre_bias;
+      ((float*)a.out)[(long)(m0 + row) * a.ldo + n0 + col] = pre_res + v;
+    }
   }
 }
 
@@ -937,9 +970,11 @@ __global__ __launch_bounds__(256) void vcap_kv_gather_kernel(const T* __restrict
 }
 
 // Per-step state init: identity page tables, cleared history / flags.
-__global__ void vcap_decode_init_kernel(int* page_table, int B, int maxp, int* finished, int* nbanned) {
+__global__ void vcap_decode_init_kernel(int* page_table, int B, int maxp, int* finished, int* nbanned, int* sk_cnt,
+                                        int n_sk) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < B * maxp) page_table[i] = i;
+  if (i < n_sk) sk_cnt[i] = 0;
   if (i < B) {
     finished[i] = 0;
     nbanned[i] = 0;
@@ -1218,13 +1253,19 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
     // f32 mlp c_proj (K = 3072 GPT-2 small / 4096 GPT-2-medium): 8 waves x 24 / 32 slabs, 16-row
     // chunks over blockIdx.y (r05: the beam searches' 24-32 rows had taken the 64-workgroup
     // generic kernel, 21 us per launch at K = 4096)
-    const dim3 grid((a.half ? 2 : 1) * ((a.N + 15) / 16), (a.M + 15) / 16);
+    const bool split = a.sk_part && a.sk_cnt && a.M <= 32 && (nsl == 48 || nsl == 64);
+    const dim3 grid((split || a.half ? 2 : 1) * ((a.N + 15) / 16), (a.M + 15) / 16);
+    if (split) {
+      if (nsl == 48) hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 12, true>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 16, true>), grid, dim3(512), 0, s, a);
+      return hipGetLastError();
+    }
     if (nsl == 48 && a.M <= 64) {
-      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 24>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 24, false>), grid, dim3(512), 0, s, a);
       return hipGetLastError();
     }
     if (nsl == 64 && a.M <= 64) {
-      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 32>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 32, false>), grid, dim3(512), 0, s, a);
       return hipGetLastError();
     }
   }
@@ -1827,10 +1868,11 @@ hipError_t vcap_kv_gather_dispatch(int dt, const void* src_pool, void* dst_pool,
   return hipGetLastError();
 }
 
-hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s) {
-  const int n = std::max(B * maxp, B);
+hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s,
+                                     int* sk_cnt, int n_sk) {
+  const int n = std::max(std::max(B * maxp, B), sk_cnt ? n_sk : 0);
   hipLaunchKernelGGL(vcap_decode_init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, page_table, B, maxp, finished,
-                     nbanned);
+                     nbanned, sk_cnt, sk_cnt ? n_sk : 0);
   return hipGetLastError();
 }
 

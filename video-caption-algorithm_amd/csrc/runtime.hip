@@ -177,6 +177,13 @@ struct DecBufs {
   int* finished;
   float* proc;        // [B][V] processed scores (sampling mode)
   unsigned* seed;     // [2] Philox key of the sampling draws
+  // f32 mlp c_proj K split (RowsGemmArgs.sk_*): pair partials + tickets.  Used only where the decode's
+  // init kernel zeroed the tickets (issue_decode sets sk_ready); other entry points keep the one-
+  // workgroup-per-tile GEMV.
+  float* skp;
+  int* skc;
+  int n_skc;
+  bool sk_ready;
 };
 
 int max_logit_blocks(int V, int B) { return vcap_logit_blocks(V, B); }
@@ -209,6 +216,11 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.proc = (float*)c.take((size_t)B * d->vocab * 4);
   b.sh = (float*)c.take((size_t)B * E * 4);
   b.seed = (unsigned*)c.take(8);
+  // K split: <= 2 row chunks of 16 (M <= 32) x E / 16 tiles x 2 halves x 256 partials; the tickets
+  b.n_skc = 2 * ((E + 15) / 16);
+  b.skp = (float*)c.take((size_t)b.n_skc * 2 * 256 * 4);
+  b.skc = (int*)c.take((size_t)b.n_skc * 4);
+  b.sk_ready = false;
   return b;
 }
 
@@ -277,6 +289,10 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     memset(&e, 0, sizeof(e));
     e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.bias = ly.mproj_b; e.N = E;
     e.K = 4 * E; e.out = w.h; e.ldo = E; e.max_blocks = max_blocks;
+    if (w.sk_ready && dt == VCAP_DT_F32 && M <= 32) {
+      e.sk_part = w.skp;
+      e.sk_cnt = w.skc;
+    }
     VCAP_TRY(vcap_rows_gemm_dispatch(dt, PRO_DIRECT, EPI_RESID, e, nullptr, s), "mlp_c_proj");
   }
   return 0;
@@ -305,13 +321,15 @@ int run_lm_head(const vcap_gpt2_desc* d, const DecBufs& w, int rows, int S_new, 
 // sp != nullptr: sampling mode (HF _sample): the lm_head also stores the processed scores, the
 // sample kernel warps them and draws (or takes force_ids), and hands the token to the finalize kernel
 int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float* prefix, const int* ids, int nids,
-                 int B, int* out_ids, float* logits_out, const DecBufs& w, int maxp, size_t page_elems,
+                 int B, int* out_ids, float* logits_out, const DecBufs& w0, int maxp, size_t page_elems,
                  hipStream_t s, const vcap_sample_params* sp = nullptr, float* warped_out = nullptr,
                  const int* force_ids = nullptr) {
   const int E = d->n_embd, V = d->vocab;
   const int P = d->prefix_len, S0 = P + nids, max_new = gp->max_new_tokens;
   const int dt = d->dtype;
-  VCAP_TRY(vcap_decode_init_dispatch(w.pt, B, maxp, w.finished, w.nbanned, s), "decode_init");
+  DecBufs w = w0;
+  w.sk_ready = true;  // the init kernel below zeroes the K-split tickets of this decode
+  VCAP_TRY(vcap_decode_init_dispatch(w.pt, B, maxp, w.finished, w.nbanned, s, w.skc, w.n_skc), "decode_init");
   VCAP_TRY(vcap_prefill_embed_dispatch(dt, prefix, P, ids, nids, d->wte, d->wpe, w.h, B, E, s), "prefill_embed");
   for (int step = 0; step < max_new; ++step) {
     const int S_new = step == 0 ? S0 : 1;

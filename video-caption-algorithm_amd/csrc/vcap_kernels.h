@@ -64,6 +64,11 @@ struct RowsGemmArgs {
   float* proc_out;  // EPI_LOGITS, optional [M, N]: the processed scores (sampling mode)
   int half;         // set by vcap_rows_gemm_dispatch: residual GEMV tiles split into two 8-column workgroups
   float* screen_h;  // lm_head stream kernel, optional [M, K] f32: workgroup 0 stores the ln_f rows it used
+  // f32 K-split residual GEMV (vcap_rows_gemv8_kernel<float, NSL, true>): per (row chunk, tile) two
+  // workgroups take one K half each; the pair meets through sk_part (2 x 256 f32 partials) and the
+  // arrival ticket sk_cnt (zeroed by vcap_decode_init at the start of every decode)
+  float* sk_part;
+  int* sk_cnt;
 };
 
 // Exact-fp32 greedy token from a bf16 lm_head screen (f32 decoders; vcap_decode_finalize_dispatch):
@@ -147,7 +152,8 @@ hipError_t vcap_decode_attention_dispatch(int dt, const void* q, const void* kc,
 hipError_t vcap_prefill_embed_dispatch(int dt, const float* prefix, int P, const int* ids, int nids, const void* wte,
                                        const float* wpe, float* h, int B, int E, hipStream_t s, int pos0 = 0,
                                        int prefix_rep = 1);
-hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s);
+hipError_t vcap_decode_init_dispatch(int* page_table, int B, int maxp, int* finished, int* nbanned, hipStream_t s,
+                                     int* sk_cnt = nullptr, int n_sk = 0);
 hipError_t vcap_decode_finalize_dispatch(int dt, const float* part_val, const int* part_idx, int nblk, int B,
                                          int step, int* finished, int* hist, int hist_ld, int* banned, int* nbanned,
                                          int ngram, int eos, int pad, int* out_ids, int out_ld, const void* wte,

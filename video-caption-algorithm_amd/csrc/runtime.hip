@@ -177,13 +177,12 @@ struct DecBufs {
   int* finished;
   float* proc;        // [B][V] processed scores (sampling mode)
   unsigned* seed;     // [2] Philox key of the sampling draws
-  // f32 mlp c_proj K split (RowsGemmArgs.sk_*): pair partials + tickets.  Used only where the decode's
-  // init kernel zeroed the tickets (issue_decode sets sk_ready); other entry points keep the one-
-  // workgroup-per-tile GEMV.
+  // f32 mlp c_proj K split (RowsGemmArgs.sk_*): pair partials + tickets, zeroed by vcap_decode_init at
+  // the start of every decode, prefill and forward_embeds sequence (all f32 paths run the same split,
+  // so a teacher-forced forward reproduces the free-running graph's logits bit for bit)
   float* skp;
   int* skc;
   int n_skc;
-  bool sk_ready;
 };
 
 int max_logit_blocks(int V, int B) { return vcap_logit_blocks(V, B); }
@@ -216,11 +215,10 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.proc = (float*)c.take((size_t)B * d->vocab * 4);
   b.sh = (float*)c.take((size_t)B * E * 4);
   b.seed = (unsigned*)c.take(8);
-  // K split: <= 2 row chunks of 16 (M <= 32) x E / 16 tiles x 2 halves x 256 partials; the tickets
-  b.n_skc = 2 * ((E + 15) / 16);
+  // K split: <= 4 row chunks of 16 (M <= 64) x E / 16 tiles x 2 halves x 256 partials; the tickets
+  b.n_skc = 4 * ((E + 15) / 16);
   b.skp = (float*)c.take((size_t)b.n_skc * 2 * 256 * 4);
   b.skc = (int*)c.take((size_t)b.n_skc * 4);
-  b.sk_ready = false;
   return b;
 }
 
@@ -289,7 +287,7 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     memset(&e, 0, sizeof(e));
     e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.bias = ly.mproj_b; e.N = E;
     e.K = 4 * E; e.out = w.h; e.ldo = E; e.max_blocks = max_blocks;
-    if (w.sk_ready && dt == VCAP_DT_F32 && M <= 32) {
+    if (dt == VCAP_DT_F32 && M <= 64) {
       e.sk_part = w.skp;
       e.sk_cnt = w.skc;
     }
@@ -327,8 +325,7 @@ int issue_decode(const vcap_gpt2_desc* d, const vcap_gen_params* gp, const float
   const int E = d->n_embd, V = d->vocab;
   const int P = d->prefix_len, S0 = P + nids, max_new = gp->max_new_tokens;
   const int dt = d->dtype;
-  DecBufs w = w0;
-  w.sk_ready = true;  // the init kernel below zeroes the K-split tickets of this decode
+  const DecBufs& w = w0;
   VCAP_TRY(vcap_decode_init_dispatch(w.pt, B, maxp, w.finished, w.nbanned, s, w.skc, w.n_skc), "decode_init");
   VCAP_TRY(vcap_prefill_embed_dispatch(dt, prefix, P, ids, nids, d->wte, d->wpe, w.h, B, E, s), "prefill_embed");
   for (int step = 0; step < max_new; ++step) {
@@ -579,7 +576,7 @@ int issue_beam(const vcap_gpt2_desc* d, const vcap_beam_params* bp, const float*
     VCAP_TRY(vcap_rows_gemm_dispatch(d->dtype, PRO_LN, EPI_LSE, g, &nblk, s), "lm_head_lse");
     return 0;
   };
-  VCAP_TRY(vcap_decode_init_dispatch(w.pt, R, bb.maxp, w.finished, w.nbanned, s), "decode_init");
+  VCAP_TRY(vcap_decode_init_dispatch(w.pt, R, bb.maxp, w.finished, w.nbanned, s, w.skc, w.n_skc), "decode_init");
   // prefill: every beam row gets its sequence's prompt (HF expands the input to B * num_beams)
   VCAP_TRY(vcap_prefill_embed_dispatch(d->dtype, prefix, d->prefix_len, ids, nids, d->wte, d->wpe, w.h, R, E, s, 0, nb),
            "prefill_embed");
@@ -1159,7 +1156,7 @@ int vcap_gpt2_prefill(const vcap_gpt2_desc* d, const float* prefix, const int* p
   void* scratch;
   if (int rc = step_setup(d, rows, S0, max_new_tokens, workspace, ws_bytes, &w, &maxp, &pe, &scratch)) return rc;
   hipStream_t s = (hipStream_t)stream;
-  VCAP_TRY(vcap_decode_init_dispatch(w.pt, rows, maxp, w.finished, w.nbanned, s), "decode_init");
+  VCAP_TRY(vcap_decode_init_dispatch(w.pt, rows, maxp, w.finished, w.nbanned, s, w.skc, w.n_skc), "decode_init");
   VCAP_TRY(vcap_prefill_embed_dispatch(d->dtype, prefix, d->prefix_len, prompt_ids, prompt_len, d->wte, d->wpe, w.h, B,
                                        d->n_embd, s),
            "prefill_embed");
@@ -1198,7 +1195,7 @@ int vcap_gpt2_forward_embeds(const vcap_gpt2_desc* d, const float* embeds, int r
   void* scratch;
   if (int rc = step_setup(d, rows, S0, max_new_tokens, workspace, ws_bytes, &w, &maxp, &pe, &scratch)) return rc;
   hipStream_t s = (hipStream_t)stream;
-  if (past_len == 0) VCAP_TRY(vcap_decode_init_dispatch(w.pt, rows, maxp, w.finished, w.nbanned, s), "decode_init");
+  if (past_len == 0) VCAP_TRY(vcap_decode_init_dispatch(w.pt, rows, maxp, w.finished, w.nbanned, s, w.skc, w.n_skc), "decode_init");
   // the prefill-embedding kernel with every position taken from `embeds` (P = n_tok, no prompt ids)
   VCAP_TRY(vcap_prefill_embed_dispatch(d->dtype, embeds, n_tok, nullptr, 0, d->wte, d->wpe, w.h, rows, d->n_embd, s,
                                        past_len),

@@ -343,7 +343,7 @@ def oracle_agreement(last, ref_ids, eos, beams: int = 1):
 
 
 STRICT_RESERVE = 32   # CUs the strict_batch leg reserves off its encode stream
-PMC_FILES = ("r05_pmc.json", "r04_pmc_colgroup.json", "r04_pmc.json", "r02_pmc.json", "r01_pmc.json")   # newest first
+PMC_FILES = ("r06_pmc.json", "r05_pmc.json", "r04_pmc_colgroup.json", "r04_pmc.json", "r02_pmc.json", "r01_pmc.json")   # newest first
 
 
 def _pmc_file(M: int):

@@ -191,8 +191,11 @@ def _launch_check(args, n: int):
         if world != n:
             return _fail(f"--gpus {n} but the launcher started WORLD_SIZE={world} ranks")
         local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
-        if not (rehearsal or args.dry_launch) and local_world > _visible_gpus():
-            return _fail(f"{local_world} ranks on this node but {_visible_gpus()} visible GPUs "
+        # this process IS a rank (torchrun started it): it may initialise HIP, so the plain device count
+        # (amdsmi, else the HIP runtime's) is the right one here
+        import torch
+        if not (rehearsal or args.dry_launch) and local_world > torch.cuda.device_count():
+            return _fail(f"{local_world} ranks on this node but {torch.cuda.device_count()} visible GPUs "
                          f"(one process per GPU; {REHEARSAL_ENV}=gloo rehearses ranks sharing GPUs)")
         return None
     if n == 1:

@@ -180,6 +180,29 @@ def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group, egroup):
         pipe.close()
 
 
+@pytest.mark.parametrize("group,egroup", [(2, 2), (4, 2)])
+def test_token_exact_pipeline_bit_identical_to_serial(device, group, egroup):
+    """The token-exact leg's schedule - bf16 ViT, fp32 GPT-2 decoder (its mlp c_proj K-split over
+    workgroup pairs, the bf16 lm_head screen) - decodes 16- and 32-row groups on two lanes with capped
+    grids beside the CU-masked encode, and every batch's ids equal a serial fp32 decode of that batch's
+    bf16 prefix: the pair hand-off and the screen are deterministic whatever the grid, lane or group."""
+    from vcap.pipeline import CaptionPipeline
+    meta, g, va, ga, sd, frames, enc, pre, _ = _models("bf16", device)
+    dec32 = HipGPT2Decoder(sd, ga, "fp32", device)
+    video = torch.from_numpy(frames).to(device)
+    _, pre_serial = enc.encode(video, pre)
+    ids_serial = dec32.generate_ids(pre_serial, [ga.bos_token_id], _hf_cfg(ga)).clone()
+    pipe = CaptionPipeline(enc, pre, dec32, _hf_cfg(ga, max_blocks=96), video.shape[0], [ga.bos_token_id], device,
+                           reserve_cus=32, dec_lanes=2, dec_group=group, enc_group=egroup)
+    try:
+        slots = [pipe.submit(video) for _ in range(2 * group + 1)]
+        pipe.synchronize()
+        for slot in slots[-group:]:
+            assert torch.equal(pipe.result(slot), ids_serial)
+    finally:
+        pipe.close()
+
+
 def test_pipelines_reuse_one_stream_set_per_schedule(device):
     """Pipelines with the same schedule reuse one set of streams for the process (vcap/pipeline.py
     _stream_set: fresh streams per pipeline measured serialised, profiles/r04_stream_reuse.txt);

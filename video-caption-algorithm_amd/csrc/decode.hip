@@ -1253,7 +1253,7 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
     // f32 mlp c_proj (K = 3072 GPT-2 small / 4096 GPT-2-medium): 8 waves x 24 / 32 slabs, 16-row
     // chunks over blockIdx.y (r05: the beam searches' 24-32 rows had taken the 64-workgroup
     // generic kernel, 21 us per launch at K = 4096)
-    const bool split = a.sk_part && a.sk_cnt && a.M <= 64 && (nsl == 48 || nsl == 64);
+    const bool split = a.sk_part && a.sk_cnt && (nsl == 48 || nsl == 64);   // any M: 16-row chunks
     const dim3 grid((split || a.half ? 2 : 1) * ((a.N + 15) / 16), (a.M + 15) / 16);
     if (split) {
       if (nsl == 48) hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 12, true>), grid, dim3(512), 0, s, a);

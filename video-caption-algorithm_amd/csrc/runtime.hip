@@ -215,8 +215,9 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.proc = (float*)c.take((size_t)B * d->vocab * 4);
   b.sh = (float*)c.take((size_t)B * E * 4);
   b.seed = (unsigned*)c.take(8);
-  // K split: <= 4 row chunks of 16 (M <= 64) x E / 16 tiles x 2 halves x 256 partials; the tickets
-  b.n_skc = 4 * ((E + 15) / 16);
+  // K split: every 16-row chunk of the largest launch (Mmax rows) x E / 16 tiles x 2 halves x 256
+  // partials; the tickets
+  b.n_skc = (int)((Mmax + 15) / 16) * ((E + 15) / 16);
   b.skp = (float*)c.take((size_t)b.n_skc * 2 * 256 * 4);
   b.skc = (int*)c.take((size_t)b.n_skc * 4);
   return b;
@@ -287,7 +288,7 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     memset(&e, 0, sizeof(e));
     e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.bias = ly.mproj_b; e.N = E;
     e.K = 4 * E; e.out = w.h; e.ldo = E; e.max_blocks = max_blocks;
-    if (dt == VCAP_DT_F32 && M <= 64) {
+    if (dt == VCAP_DT_F32) {  // every row count: the f32 arithmetic may not depend on the launch's M
       e.sk_part = w.skp;
       e.sk_cnt = w.skc;
     }

@@ -88,6 +88,23 @@ def patch_decode(s: str) -> str:
     att = att[:att.rindex("}")] + "  if (threadIdx.x == 0) vcap_stamp_rec(0xA000ull, t0, t1, t1, t1, t1, VCAP_RT());\n}\n\n"
     assert att.count("VCAP_RT()") == 3, att.count("VCAP_RT()")
     s = s[:a0] + att + s[a1:]
+    # lm_head stream kernel (greedy / screen): entry | ln_f tile in LDS (+ flags) | first column group
+    # done | second group done | last group done | argmax partials written  (tag 0xC000)
+    l0 = s.index("__global__ __launch_bounds__(256) void vcap_lm_head_stream_kernel(RowsGemmArgs a, int tpw) {")
+    l1 = s.index("template <typename T, int NSL>\nstatic bool launch_lm_stream", l0)
+    lm = s[l0:l1]
+    lm = lm.replace("  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n",
+                    "  const unsigned long long st0 = VCAP_RT();\n  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n", 1)
+    lm = lm.replace("  __syncthreads();  // flags zeroed, A tile written\n",
+                    "  __syncthreads();  // flags zeroed, A tile written\n  const unsigned long long st1 = VCAP_RT();\n"
+                    "  unsigned long long st2 = 0, st3 = 0;\n", 1)
+    lm = lm.replace("    group(wA, gi);\n", "    group(wA, gi);\n    if (gi == 0) st2 = VCAP_RT();\n", 1)
+    lm = lm.replace("      group(wB, gi + 1);\n", "      group(wB, gi + 1);\n      if (gi == 0) st3 = VCAP_RT();\n", 1)
+    lm = lm.replace("  argmax_take(bv_run, bi_run, dpp_f<DPP_XOR1>(bv_run), dpp_i<DPP_XOR1>(bi_run));\n",
+                    "  const unsigned long long st4 = VCAP_RT();\n  argmax_take(bv_run, bi_run, dpp_f<DPP_XOR1>(bv_run), dpp_i<DPP_XOR1>(bi_run));\n", 1)
+    lm = lm[:lm.rindex("}")] + "  if (threadIdx.x == 0) vcap_stamp_rec(0xC000ull, st0, st1, st2, st3 ? st3 : st2, st4, VCAP_RT());\n}\n\n"
+    assert lm.count("VCAP_RT()") == 6, lm.count("VCAP_RT()")
+    s = s[:l0] + lm + s[l1:]
     return s
 
 

@@ -34,6 +34,8 @@ ROLE = {0x0: "c_attn(LN+QKV)", 0x2: "c_fc(LN+GELU)", 0x1: "c_proj(+res)", 0x3: "
 def role(tag):
     if tag == 0xA000:
         return "attention"
+    if tag == 0xC000:   # act = ln_f tile ready, wgt = 1st column group, mfma = 2nd, red = the rest, epi = partials
+        return "lm_head stream (act=LN, wgt=group0, mfma=group1, red=rest, epi=partials)"
     epi, pro, nsl = (tag >> 8) & 0xF, (tag >> 4) & 0xF, (tag >> 12) & 0xFF
     name = {0: "c_attn(LN+QKV)", 2: "c_fc(LN+GELU)", 1: "c_proj(+res)", 3: "lm_head(LN+proc)"}.get(epi, f"epi{epi}")
     return f"{name} nsl{nsl}" + (" half" if (tag >> 24) & 1 else "")

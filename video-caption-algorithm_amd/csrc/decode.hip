@@ -380,12 +380,18 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   // the weights of 8 columns (lanes l and l ^ 8 load the same fragment: column (l & 7) of its half),
   // so a K = 3072 projection spreads its weight stream over twice the CUs; the MFMAs, their order
   // and every stored output are those of the full-tile workgroup
-  const bool half = EPI == EPI_RESID && NTB == 1 && a.half;
+  // a.sk_part (the bf16 mlp c_proj, r06): K split over a workgroup pair per 16-column tile and 16-row
+  // chunk, each workgroup one K half of the whole tile - half the activation rows per workgroup, the
+  // pair meeting as in vcap_rows_gemv8_kernel<float, NSL, true>
+  constexpr bool CAN_SPLIT = EPI == EPI_RESID && NTB == 1 && MT == 1 && PRO == PRO_DIRECT;
+  const bool split = CAN_SPLIT && a.sk_part != nullptr;
+  const bool half = EPI == EPI_RESID && NTB == 1 && a.half && !split;
   const int hsel = half ? (int)(blockIdx.x & 1) : -1;
-  const int n0 = half ? (int)(blockIdx.x >> 1) * 16 : blockIdx.x * NTB * 16;
+  const int ksel = split ? (int)(blockIdx.x & 1) : 0;
+  const int n0 = (half || split) ? (int)(blockIdx.x >> 1) * 16 : blockIdx.x * NTB * 16;
   const int wlane = half ? ((lane & 0x30) | (hsel << 3) | (lane & 7)) : lane;
-  const int nslab = 4 * NSL;  // = K / KS
-  const int g0 = wave * NSL;
+  const int nslab = (split ? 8 : 4) * NSL;  // = K / KS
+  const int g0 = (split ? ksel * 4 * NSL : 0) + wave * NSL;
   const int ntiles = (N + 15) >> 4;
 
   if constexpr (EPI == EPI_LOGITS) proc_flags_zero<MP, NTB>(s_rep, s_ban);
@@ -536,6 +542,30 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
       for (int r = 0; r < 4; ++r) red[wave][(i * NTB + j) * 256 + (fg * 4 + r) * 16 + fr] = acc[i][j][r];
   if constexpr (EPI == EPI_LOGITS) toks.template mark<NTB>(a, m0, n0, s_rep, s_ban);
   __syncthreads();
+  if constexpr (CAN_SPLIT) {
+    if (split) {
+      // the pair hand-off (MI355X guide Guideline 16 R1): sc1 partial stores drained by every storing
+      // wave before the barrier, one agent-scope ticket, the second arriver's sc1 loads; the sum is
+      // p(K half 0) + p(K half 1) in that order whichever workgroup arrives second
+      __shared__ int s_ticket;
+      const long pair = (long)blockIdx.y * (gridDim.x >> 1) + (blockIdx.x >> 1);
+      const float part = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+      __hip_atomic_store(a.sk_part + (pair * 2 + ksel) * 256 + tid, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) s_ticket = __hip_atomic_fetch_add(a.sk_cnt + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if ((s_ticket & 1) == 0) return;
+      const int m = m0 + (tid >> 4), n = n0 + (tid & 15);
+      if (m < M && n < N) {
+        const float other =
+            __hip_atomic_load(a.sk_part + (pair * 2 + (ksel ^ 1)) * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float v = (ksel == 0 ? part + other : other + part) + pre_bias[0];
+        ((float*)a.out)[(long)m * a.ldo + n] = pre_res[0] + v;
+      }
+      return;
+    }
+  }
   rows_epilogue<T, MT, NTB, EPI>(a, m0, red, pre_bias, pre_res, lg, s_rep, s_ban, n0, hsel);
 }
 
@@ -1178,7 +1208,8 @@ constexpr size_t kRowsLdsMax = 160 * 1024;  // LDS per CU (static + dynamic)
 
 template <typename T>
 constexpr bool gemv_nsl_ok(int nsl) {
-  return sizeof(T) == 2 ? (nsl == 6 || nsl == 8 || nsl == 24 || nsl == 32) : (nsl == 12 || nsl == 16);
+  return sizeof(T) == 2 ? (nsl == 6 || nsl == 8 || nsl == 12 || nsl == 16 || nsl == 24 || nsl == 32)
+                        : (nsl == 12 || nsl == 16);
 }
 // register budget: NSL x (NTB weight + MT activation) 16-byte fragments held at once
 // (a 32-row PRO_DIRECT GEMV whose two row tiles of A fragments do not fit beside the weights streams
@@ -1206,7 +1237,7 @@ static int allow_lds(Kern k, int& limit) {
 
 template <typename T, int MT, int NTB, int PRO, int EPI, int NSL>
 static hipError_t launch_gemv(const RowsGemmArgs& a, hipStream_t s) {
-  const int half = EPI == EPI_RESID && NTB == 1 && a.half ? 2 : 1;
+  const int half = EPI == EPI_RESID && NTB == 1 && (a.half || a.sk_part) ? 2 : 1;
   const dim3 grid(half * ((a.N + NTB * 16 - 1) / (NTB * 16)), (a.M + MT * 16 - 1) / (MT * 16));
   const size_t lds = PRO == PRO_LN ? (size_t)MT * 16 * a.K * sizeof(T) : 0;
   static int limit = 0;
@@ -1243,7 +1274,10 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
   if ((long)(a.N + 63) * a.K * (long)sizeof(T) >= 0x7FFFFFFFL ||
       (long)a.M * a.ldx * (long)(PRO == PRO_LN ? sizeof(float) : sizeof(T)) >= 0x7FFFFFFFL)
     return hipErrorInvalidValue;
-  const int nsl = a.K / (16 * Frag<T>::kElems);
+  // the bf16 K-split residual GEMV (a.sk_part; the dispatcher sends it in 16-row chunks): each workgroup
+  // streams half the slabs
+  const bool ksplit = sizeof(T) == 2 && a.sk_part && MT == 1 && NTB == 1 && PRO == PRO_DIRECT && EPI == EPI_RESID;
+  const int nsl = a.K / (16 * Frag<T>::kElems) / (ksplit ? 2 : 1);
   hipError_t err = hipSuccess;
   if (try_gemv<T, MT, NTB, PRO, EPI, 6>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 8>(nsl, a, s, err) ||
       try_gemv<T, MT, NTB, PRO, EPI, 12>(nsl, a, s, err) || try_gemv<T, MT, NTB, PRO, EPI, 16>(nsl, a, s, err) ||
@@ -1719,7 +1753,18 @@ hipError_t vcap_rows_gemm_dispatch(int dt, int pro, int epi, const RowsGemmArgs&
   // f32 LayerNorm-prologue rows of > 512 features in 32-row chunks would need > 64 KiB of A tile
   // beside the split-K buffers (GPT-2-medium fp32 beam search: 32 x 1024 x 4 B + 32 KiB > 160 KiB):
   // such launches take 16-row chunks (two blockIdx.y chunks per 32 rows)
-  const bool one = a.M <= 16 || (pro == PRO_LN && dt != VCAP_DT_BF16 && a.K > 512);
+  // the bf16 mlp c_proj K split (GPT-2 small's K = 3072, whole tiles) runs in 16-row chunks at every row
+  // count; elsewhere a bf16 launch ignores sk_part.  (GPT-2-medium's K = 4096 keeps the one-workgroup
+  // tile in bf16: its device beam search is priced against the reference's hypotheses under fp32
+  // (test_l14_medium_beam4_bf16_priced_against_reference), and a beam search's path moves with any
+  // change of bf16 summation order.)
+  if (dt == VCAP_DT_BF16 && ah.sk_part &&
+      !(pro == PRO_DIRECT && epi == EPI_RESID && ntb == 1 && a.K == 3072)) {
+    ah.sk_part = nullptr;
+    ah.sk_cnt = nullptr;
+  }
+  const bool bsplit = dt == VCAP_DT_BF16 && ah.sk_part;
+  const bool one = a.M <= 16 || bsplit || (pro == PRO_LN && dt != VCAP_DT_BF16 && a.K > 512);
 #define VCAP_ROWS(TT, PP, EE, NT) \
   return one ? launch_rows<TT, 1, NT, PP, EE>(ah, s) : launch_rows<TT, 2, NT, PP, EE>(ah, s);
 #define VCAP_ROWS_NT(TT, PP, EE)            \

@@ -288,7 +288,8 @@ int run_layers(const vcap_gpt2_desc* d, const DecBufs& w, int maxp, size_t page_
     memset(&e, 0, sizeof(e));
     e.M = M; e.x = w.act; e.ldx = 4 * E; e.w = ly.mproj_w; e.bias = ly.mproj_b; e.N = E;
     e.K = 4 * E; e.out = w.h; e.ldo = E; e.max_blocks = max_blocks;
-    if (dt == VCAP_DT_F32) {  // every row count: the f32 arithmetic may not depend on the launch's M
+    {  // every row count: the arithmetic may not depend on the launch's M (the dispatcher drops the split where
+       // it does not apply)
       e.sk_part = w.skp;
       e.sk_cnt = w.skc;
     }

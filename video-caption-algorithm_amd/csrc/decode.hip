@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
   // and every stored output are those of the full-tile workgroup
   // a.sk_part (the bf16 mlp c_proj, r06): K split over a workgroup pair per 16-column tile and 16-row
   // chunk, each workgroup one K half of the whole tile - half the activation rows per workgroup, the
-  // pair meeting as in vcap_rows_gemv8_kernel<float, NSL, true>
+  // pair meeting as in vcap_rows_gemv8_kernel<float, NSL, 2, 1>
   constexpr bool CAN_SPLIT = EPI == EPI_RESID && NTB == 1 && MT == 1 && PRO == PRO_DIRECT;
   const bool split = CAN_SPLIT && a.sk_part != nullptr;
   const bool half = EPI == EPI_RESID && NTB == 1 && a.half && !split;
@@ -579,12 +579,14 @@ __global__ __launch_bounds__(256) void vcap_rows_gemv_kernel(RowsGemmArgs a) {
 // once too; past that (NSL = 32: 128 weight + 128 A registers would not fit the 256 of a 2-wave
 // SIMD) they come in batches of 8 slabs, two batches live, batch b + 2 issued once batch b's
 // MFMAs have consumed its registers (the activation rows are L2-resident: every workgroup reads them).
-template <typename T, int NSL, bool SPLIT>
+template <typename T, int NSL, int KP, int NT>
 __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
   constexpr int E = Frag<T>::kElems, KS = 4 * E;
   constexpr int AB = NSL <= 24 ? NSL : 8, NAB = NSL / AB;
+  constexpr bool SPLIT = KP > 1;
   static_assert(NSL % AB == 0, "A batches tile the wave's slabs");
-  __shared__ __attribute__((aligned(16))) float red[8][256];
+  static_assert(NT == 1 || (KP == 4 && NT == 2), "column-tile pairs only with the 4-way K split");
+  __shared__ __attribute__((aligned(16))) float red[8][NT * 256];
   __shared__ int s_ticket;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
@@ -592,15 +594,18 @@ __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
   const int m0 = blockIdx.y * 16;
   // a.half: two workgroups per 16-column tile, each streaming 8 columns' weights (as in
   // vcap_rows_gemv_kernel: lanes l and l ^ 8 load the same fragment), the stores of its 8 columns.
-  // SPLIT: two workgroups per 16-column tile, each taking one half of K for all 16 columns, so each
-  // ingests half the activation rows (the f32 mlp c_proj's 196 KiB of activations per workgroup was
-  // twice its weight slice: profiles/r06_decode_stamps.txt); the pair meets below.
+  // SPLIT (KP K parts): KP workgroups per group of NT 16-column tiles, each taking one K part for all
+  // the group's columns, so each ingests 1/KP of the activation rows (the f32 mlp c_proj's 196 KiB of
+  // activations per workgroup was twice its weight slice: profiles/r06_decode_stamps.txt).  KP = 2,
+  // NT = 1: 98 KiB of activations + 98 KiB of weights per workgroup; KP = 4, NT = 2 (GPT-2 small, r06
+  // late): 49 + 98 KiB, the same workgroup count.  The K parts meet below.
   const bool half = !SPLIT && a.half != 0;
   const int hsel = half ? (int)(blockIdx.x & 1) : -1;
-  const int ksel = SPLIT ? (int)(blockIdx.x & 1) : 0;
-  const int n0 = (half || SPLIT) ? (int)(blockIdx.x >> 1) * 16 : (int)blockIdx.x * 16;
+  const int ksel = SPLIT ? (int)(blockIdx.x % KP) : 0;
+  const int grp = SPLIT ? (int)(blockIdx.x / KP) : (int)blockIdx.x;
+  const int n0 = half ? (int)(blockIdx.x >> 1) * 16 : grp * 16 * NT;
   const int wlane = half ? ((lane & 0x30) | (hsel << 3) | (lane & 7)) : lane;
-  const int nslab = (SPLIT ? 16 : 8) * NSL, g0 = (SPLIT ? ksel * 8 * NSL : 0) + wave * NSL;
+  const int nslab = KP * 8 * NSL, g0 = ksel * 8 * NSL + wave * NSL;
   const int ntiles = (N + 15) >> 4;
   u32x4 af[NAB > 1 ? 2 : 1][AB];
   const long xo = (long)min(m0 + fr, M - 1) * a.ldx + fg * E;
@@ -611,22 +616,31 @@ __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
   };
   aload(0);
   asm volatile("" ::: "memory");  // the activation loads issue before the weights
-  u32x4 wf[NSL];
-  const u32x4* wp = packed_frag(a.w, min(n0 / 16, ntiles - 1), nslab, g0, wlane);
+  u32x4 wf[NSL][NT];
 #pragma unroll
-  for (int s = 0; s < NSL; ++s) wf[s] = vcap_dec_wload<true>(a.w, wp + s * 64);
+  for (int j = 0; j < NT; ++j) {
+    const u32x4* wp = packed_frag(a.w, min(n0 / 16 + j, ntiles - 1), nslab, g0, wlane);
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) wf[s][j] = vcap_dec_wload<true>(a.w, wp + s * 64);
+  }
   if constexpr (NAB > 1) aload(1);
-  const int row = (tid >> 4) & 15, col = tid & 15;
-  const int mc = min(m0 + row, M - 1), nc = min(n0 + col, N - 1);
+  // this thread's output element: tile tj, row, col (NT = 2: all 512 threads; NT = 1: the first 256)
+  const int tj = NT == 2 ? (tid >> 8) : 0, e = tid & 255;
+  const int row = e >> 4, col = e & 15;
+  const int mc = min(m0 + row, M - 1), nc = min(n0 + tj * 16 + col, N - 1);
   const float bl = *(a.bias ? a.bias + nc : (const float*)a.x);
   const float pre_bias = a.bias ? bl : 0.f;
   const float pre_res = ((const float*)a.out)[(long)mc * a.ldo + nc];
   asm volatile("" : "+v"(af[0][0])::"memory");
-  f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int b = 0; b < NAB; ++b) {
 #pragma unroll
-    for (int s = 0; s < AB; ++s) acc = mfma_frag(af[b & 1][s], wf[b * AB + s], acc, (T*)nullptr);
+    for (int s = 0; s < AB; ++s)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = mfma_frag(af[b & 1][s], wf[b * AB + s][j], acc[j], (T*)nullptr);
     if (b + 2 < NAB) {
       // batch b consumed before its registers reload, and the batch's 8 loads issue together (the
       // scheduler otherwise sinks each to its use: 8 serial L2 round trips)
@@ -636,39 +650,47 @@ __global__ __launch_bounds__(512) void vcap_rows_gemv8_kernel(RowsGemmArgs a) {
     }
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) red[wave][(fg * 4 + r) * 16 + fr] = acc[r];
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][j * 256 + (fg * 4 + r) * 16 + fr] = acc[j][r];
   __syncthreads();
+  const bool mine = tid < NT * 256;
+  const int ei = tj * 256 + e;
   if constexpr (SPLIT) {
-    // The K-half partials of a tile meet through global memory, the MI355X guide's valid hand-off
-    // form (Guideline 16 R1): every partial store is sc1 (agent-scope relaxed atomic store: write-
-    // through) and every storing wave drains (vmcnt(0)) before the workgroup barrier; then one lane
-    // takes a ticket (agent-scope atomic add, zeroed per decode by vcap_decode_init).  The pair's
-    // second arriver loads the other half's partial with sc1 loads and stores the output; the first
-    // exits.  Neither waits for the other (no spin), and the sum is p(K half 0) + p(K half 1) whichever
-    // arrives first, so the result is deterministic.
-    const long pair = (long)blockIdx.y * (gridDim.x >> 1) + (blockIdx.x >> 1);
+    // The K-part partials of a column group meet through global memory, the MI355X guide's valid
+    // hand-off form (Guideline 16 R1): every partial store is sc1 (agent-scope relaxed atomic store:
+    // write-through) and every storing wave drains (vmcnt(0)) before the workgroup barrier; then one
+    // lane takes a ticket (agent-scope atomic add, zeroed per decode by vcap_decode_init; KP per group
+    // per launch).  The group's last arriver loads the other parts' partials with sc1 loads and stores
+    // the output; the others exit.  No one waits (no spin), and the sum is
+    // ((p0 + p1) + (p2 + p3)) (KP = 4) or p0 + p1 (KP = 2) whichever arrives last: deterministic.
+    const long g = (long)blockIdx.y * (gridDim.x / KP) + grp;
     float part = 0.f;
-    if (tid < 256) {
-      const int e = tid;
-      part = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) + ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e]));
-      __hip_atomic_store(a.sk_part + (pair * 2 + ksel) * 256 + e, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (mine) {
+      part = ((red[0][ei] + red[1][ei]) + (red[2][ei] + red[3][ei])) + ((red[4][ei] + red[5][ei]) + (red[6][ei] + red[7][ei]));
+      __hip_atomic_store(a.sk_part + ((g * KP + ksel) * NT) * 256 + ei, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
-    if (tid == 0) s_ticket = __hip_atomic_fetch_add(a.sk_cnt + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) s_ticket = __hip_atomic_fetch_add(a.sk_cnt + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if ((s_ticket & 1) == 0) return;  // first of the pair (tickets advance by 2 per launch)
-    if (tid < 256 && m0 + row < M && n0 + col < N) {
-      const float other =
-          __hip_atomic_load(a.sk_part + (pair * 2 + (ksel ^ 1)) * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float v = (ksel == 0 ? part + other : other + part) + pre_bias;
-      ((float*)a.out)[(long)(m0 + row) * a.ldo + n0 + col] = pre_res + v;
+    if ((s_ticket % KP) != KP - 1) return;  // not the last of the group (tickets advance by KP per launch)
+    if (mine && m0 + row < M && n0 + tj * 16 + col < N) {
+      float p[KP];
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+        p[k] = k == ksel ? part
+                         : __hip_atomic_load(a.sk_part + ((g * KP + k) * NT) * 256 + ei, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      float v;
+      if constexpr (KP == 4) v = (p[0] + p[1]) + (p[2] + p[3]);
+      else v = p[0] + p[1];
+      ((float*)a.out)[(long)(m0 + row) * a.ldo + n0 + tj * 16 + col] = pre_res + (v + pre_bias);
     }
   } else {
-    if (tid < 256 && m0 + row < M && n0 + col < N && (hsel < 0 || (col >> 3) == hsel)) {
-      const int e = tid;
-      const float v = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) +
-                      ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e])) + pre_bias;
+    if (mine && m0 + row < M && n0 + col < N && (hsel < 0 || (col >> 3) == hsel)) {
+      const float v = ((red[0][ei] + red[1][ei]) + (red[2][ei] + red[3][ei])) +
+                      ((red[4][ei] + red[5][ei]) + (red[6][ei] + red[7][ei])) + pre_bias;
       ((float*)a.out)[(long)(m0 + row) * a.ldo + n0 + col] = pre_res + v;
     }
   }
@@ -1289,17 +1311,22 @@ static hipError_t launch_rows(const RowsGemmArgs& a, hipStream_t s) {
     // generic kernel, 21 us per launch at K = 4096)
     const bool split = a.sk_part && a.sk_cnt && (nsl == 48 || nsl == 64);   // any M: 16-row chunks
     const dim3 grid((split || a.half ? 2 : 1) * ((a.N + 15) / 16), (a.M + 15) / 16);
+    if (split && nsl == 48 && a.N % 32 == 0) {
+      // GPT-2 small: 4 K parts x 2-column-tile groups (the same workgroup count as the pairs)
+      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 6, 4, 2>), grid, dim3(512), 0, s, a);
+      return hipGetLastError();
+    }
     if (split) {
-      if (nsl == 48) hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 12, true>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 16, true>), grid, dim3(512), 0, s, a);
+      if (nsl == 48) hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 12, 2, 1>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 16, 2, 1>), grid, dim3(512), 0, s, a);
       return hipGetLastError();
     }
     if (nsl == 48 && a.M <= 64) {
-      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 24, false>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 24, 1, 1>), grid, dim3(512), 0, s, a);
       return hipGetLastError();
     }
     if (nsl == 64 && a.M <= 64) {
-      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 32, false>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((vcap_rows_gemv8_kernel<float, 32, 1, 1>), grid, dim3(512), 0, s, a);
       return hipGetLastError();
     }
   }

@@ -215,10 +215,11 @@ DecBufs carve_dec(Carver& c, const vcap_gpt2_desc* d, int B, int S0, int max_new
   b.proc = (float*)c.take((size_t)B * d->vocab * 4);
   b.sh = (float*)c.take((size_t)B * E * 4);
   b.seed = (unsigned*)c.take(8);
-  // K split: every 16-row chunk of the largest launch (Mmax rows) x E / 16 tiles x 2 halves x 256
-  // partials; the tickets
+  // K split: every 16-row chunk of the largest launch (Mmax rows) x E / 16 tiles x 256 partials x 4
+  // (the pairs: 2 halves per tile; the f32 4-way split: E / 32 groups x 4 parts x 2 tiles); the
+  // tickets, one per tile or group
   b.n_skc = (int)((Mmax + 15) / 16) * ((E + 15) / 16);
-  b.skp = (float*)c.take((size_t)b.n_skc * 2 * 256 * 4);
+  b.skp = (float*)c.take((size_t)b.n_skc * 4 * 256 * 4);
   b.skc = (int*)c.take((size_t)b.n_skc * 4);
   return b;
 }

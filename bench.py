@@ -85,6 +85,10 @@ def parse():
                     help="consecutive batches encoded together as one encode (divides --dec-group); 0 = auto: "
                          "2 while a batch holds <= 128 frames (the N = 768 GEMMs of one 8 x 16-frame batch fill "
                          "1.16 rounds of 256 tiles), else 1")
+    ap.add_argument("--decode-cus", type=int, default=-1,
+                    help="mask the decode lanes to the first N CUs (the reserved ones + N - reserve of the encode's); "
+                         "0: unmasked; -1 (auto): 96 for a bf16, 160 for an fp32 greedy decoder beside a CU-reserved "
+                         "encode, else 0")
     ap.add_argument("--confine-decode", action="store_true",
                     help="mask the decode streams to the reserved CUs (default: unmasked, high priority)")
     ap.add_argument("--gemm-policy", type=int, default=0, help="vcap_set_gemm_policy value for A/B runs (0 = auto)")
@@ -468,6 +472,21 @@ def parity_report(sd, va, ga, video, pre, enc, dec, cfg, last, dev):
     return rep
 
 
+# Decode lanes masked to the first N CUs (the 32 the encode leaves free + N - 32 of the encode's): the
+# decode's workgroups then never land on the other encode CUs between two GEMM workgroups.  Measured
+# (profiles/r06_decode_cus_sweep.txt, same box, interleaved): bf16 decoder unmasked 1246.7-1249.1,
+# 64 CUs 1268.3-1269.1, 96 CUs 1269.7-1271.8, 128 CUs 1261.8-1264.3, 160 CUs 1258.6-1259.7 captions/s
+# (p50 28.4 -> 30.9 ms at 96); fp32 decoder unmasked 1180.7-1181.5, 64 CUs 1016.4-1016.8 (the decode
+# becomes the bottleneck), 128 CUs 1176.2-1177.7, 160 CUs 1193.0-1193.1.
+DECODE_CUS = {"bf16": 96, "fp32": 160}
+
+
+def auto_decode_cus(args, dec_precision: str) -> int:
+    if args.serial or args.confine_decode or args.reserve_cus <= 0 or args.beams != 1 or args.precision != "bf16":
+        return 0
+    return DECODE_CUS.get(dec_precision, 0)
+
+
 def time_schedule(enc, pre, dec, cfg, video, prompt, dev, world, steps, warmup, keep_last=False, **sched):
     """Time `steps` batches of `video` through a fresh CaptionPipeline with the given schedule,
     bracketed like the headline (synchronize + barrier on both sides, max over ranks): captions/s,
@@ -614,6 +633,9 @@ def main():
     pre = HipPrefix(sd, ga.n_embd, device=dev)
     if args.dec_precision == "auto":
         args.dec_precision = "fp32" if args.precision == "fp32" else "bf16"
+    decode_cus_auto = args.decode_cus < 0
+    if decode_cus_auto:
+        args.decode_cus = auto_decode_cus(args, args.dec_precision)
     dec = HipGPT2Decoder(sd, ga, args.dec_precision, dev, screen=args.lm_screen == "on")
     if args.decode == "hf_greedy":
         cfg = GenConfig(args.max_new, 8, 3, 1.1, ga.eos_token_id, ga.eos_token_id, not args.no_graph,
@@ -638,7 +660,8 @@ def main():
                            else None,
                            reserve_cus=0 if args.serial else args.reserve_cus,
                            dec_lanes=1 if args.serial else args.dec_lanes,
-                           confine_decode=args.confine_decode and not args.serial,
+                           confine_decode=False if args.serial else (args.decode_cus if args.decode_cus > 0
+                                                                      else args.confine_decode),
                            dec_group=1 if args.serial else args.dec_group,
                            enc_group=1 if args.serial else args.enc_group)
 
@@ -733,13 +756,18 @@ def main():
         dec32 = HipGPT2Decoder(sd, ga, "fp32", dev, screen=args.lm_screen == "on")
         token_exact = time_schedule(enc, pre, dec32, cfg, video, prompt, dev, world, te_steps, args.warmup,
                                     keep_last=True, dec_lanes=args.dec_lanes, dec_group=args.dec_group,
-                                    enc_group=args.enc_group, reserve_cus=args.reserve_cus)
+                                    enc_group=args.enc_group, reserve_cus=args.reserve_cus,
+                                    confine_decode=auto_decode_cus(args, "fp32") if decode_cus_auto
+                                    else args.decode_cus)
         lat_t, vit_t, dec_t = token_exact.pop("_per_batch_ms")
         token_exact["stage_ms_p50"] = {"vit_encode_prefix": statistics.median(vit_t),
                                        "prefix_ready_to_ids": statistics.median(dec_t)}
         token_exact["precision"] = "ViT bf16 + GPT-2 decoder fp32 (bf16 lm_head screen + exact f32 rescoring)" \
             if dec32.screen else "ViT bf16 + GPT-2 decoder fp32"
-        token_exact["schedule"] = "the headline's (same lanes, groups, CU reservation and decode grid cap)"
+        token_exact["decode_cus"] = auto_decode_cus(args, "fp32") if decode_cus_auto else args.decode_cus
+        token_exact["schedule"] = ("the headline's (same lanes, groups, CU reservation and decode grid cap); decode "
+                                   f"lanes masked to {token_exact['decode_cus']} CUs" if token_exact["decode_cus"]
+                                   else "the headline's (same lanes, groups, CU reservation and decode grid cap)")
         if args.decode_alone:
             with torch.cuda.stream(torch.cuda.Stream(dev)):
                 _, pre_a = enc.encode(video, pre)
@@ -859,7 +887,11 @@ def main():
                        f"lane(s) in flight; each encode = {args.enc_group} consecutive batch(es) as one "
                        f"{args.enc_group * B}-video encode; each decode = {args.dec_group} consecutive batch(es) as one "
                        + (f"{args.dec_group * B}-row greedy decode graph" if args.beams == 1 else
-                          f"{args.dec_group * B} x {args.beams}-beam search graph"),
+                          f"{args.dec_group * B} x {args.beams}-beam search graph")
+                       + (f"; decode lanes masked to {args.decode_cus} CUs (the {args.reserve_cus} the encode leaves "
+                          f"free + {args.decode_cus - args.reserve_cus} of its)" if args.decode_cus > 0 and not args.serial
+                          else ""),
+                       "decode_cus": 0 if args.serial else args.decode_cus,
                        "dec_lanes": 1 if args.serial else args.dec_lanes,
                        "dec_group": 1 if args.serial else args.dec_group,
                        "enc_group": 1 if args.serial else args.enc_group},

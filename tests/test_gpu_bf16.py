@@ -155,13 +155,15 @@ def test_lm_head_processor_epilogue_every_step(device, prec):
         fin |= ids64[:, s] == eos
 
 
-@pytest.mark.parametrize("lanes,group,egroup", [(2, 1, 1), (1, 2, 1), (2, 2, 1), (1, 4, 1), (2, 2, 2), (1, 4, 2)])
-def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group, egroup):
+@pytest.mark.parametrize("lanes,group,egroup,dcus", [(2, 1, 1, 0), (1, 2, 1, 0), (2, 2, 1, 0), (1, 4, 1, 0),
+                                                     (2, 2, 2, 0), (1, 4, 2, 0), (2, 2, 2, 96)])
+def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group, egroup, dcus):
     """The bench schedule (vcap/pipeline.py: CU-masked encode stream, decode lanes with capped
     grids, own workspaces / graphs, optionally `group` batches decoded as one decode of group*8
-    rows and `egroup` batches encoded as one encode of egroup*8 videos) gives bit-identical bf16
-    encodes and ids to a serial bf16 encode + generate_ids of one batch on the default stream
-    (deterministic, M-independent split-K; mask-independent plans; row-independent kernels)."""
+    rows and `egroup` batches encoded as one encode of egroup*8 videos, and the decode lanes masked
+    to the first `dcus` CUs as the headline runs them) gives bit-identical bf16 encodes and ids to a
+    serial bf16 encode + generate_ids of one batch on the default stream (deterministic,
+    M-independent split-K; mask-independent plans; row-independent kernels)."""
     from vcap.pipeline import CaptionPipeline
     meta, g, va, ga, sd, frames, enc, pre, dec = _models("bf16", device)
     video = torch.from_numpy(frames).to(device)
@@ -169,7 +171,7 @@ def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group, egroup):
     ids_serial = dec.generate_ids(pre_serial, [ga.bos_token_id], _hf_cfg(ga)).clone()
     cfg = _hf_cfg(ga, max_blocks=128)
     pipe = CaptionPipeline(enc, pre, dec, cfg, video.shape[0], [ga.bos_token_id], device, reserve_cus=32,
-                           dec_lanes=lanes, dec_group=group, enc_group=egroup)
+                           dec_lanes=lanes, dec_group=group, enc_group=egroup, confine_decode=dcus)
     try:
         slots = [pipe.submit(video) for _ in range(5)]
         pipe.synchronize()
@@ -180,12 +182,13 @@ def test_bf16_pipeline_bit_identical_to_serial(device, lanes, group, egroup):
         pipe.close()
 
 
-@pytest.mark.parametrize("group,egroup", [(2, 2), (4, 2)])
-def test_token_exact_pipeline_bit_identical_to_serial(device, group, egroup):
+@pytest.mark.parametrize("group,egroup,dcus", [(2, 2, 0), (4, 2, 0), (2, 2, 160)])
+def test_token_exact_pipeline_bit_identical_to_serial(device, group, egroup, dcus):
     """The token-exact leg's schedule - bf16 ViT, fp32 GPT-2 decoder (its mlp c_proj K-split over
     workgroup pairs, the bf16 lm_head screen) - decodes 16- and 32-row groups on two lanes with capped
     grids beside the CU-masked encode, and every batch's ids equal a serial fp32 decode of that batch's
-    bf16 prefix: the pair hand-off and the screen are deterministic whatever the grid, lane or group."""
+    bf16 prefix: the pair hand-off and the screen are deterministic whatever the grid, lane, group or
+    decode CU mask (160 CUs: the token-exact leg's)."""
     from vcap.pipeline import CaptionPipeline
     meta, g, va, ga, sd, frames, enc, pre, _ = _models("bf16", device)
     dec32 = HipGPT2Decoder(sd, ga, "fp32", device)
@@ -193,7 +196,7 @@ def test_token_exact_pipeline_bit_identical_to_serial(device, group, egroup):
     _, pre_serial = enc.encode(video, pre)
     ids_serial = dec32.generate_ids(pre_serial, [ga.bos_token_id], _hf_cfg(ga)).clone()
     pipe = CaptionPipeline(enc, pre, dec32, _hf_cfg(ga, max_blocks=96), video.shape[0], [ga.bos_token_id], device,
-                           reserve_cus=32, dec_lanes=2, dec_group=group, enc_group=egroup)
+                           reserve_cus=32, dec_lanes=2, dec_group=group, enc_group=egroup, confine_decode=dcus)
     try:
         slots = [pipe.submit(video) for _ in range(2 * group + 1)]
         pipe.synchronize()

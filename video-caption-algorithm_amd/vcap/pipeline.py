@@ -28,7 +28,7 @@ so a video's prefix - and its caption - is bit-identical whichever batch it is e
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Union
 
 import atexit
 import ctypes as C
@@ -55,9 +55,12 @@ def _device_index(device) -> int:
     return d.index if d.index is not None else torch.cuda.current_device()
 
 
-def _stream_set(device, reserve_cus: int, confine_decode: bool, lanes: int):
+def _stream_set(device, reserve_cus: int, confine_decode, lanes: int):
+    """confine_decode: False = decode lanes unmasked; True = masked to the reserved CUs; an int n > 1 =
+    masked to the first n CUs (the reserved ones plus n - reserve_cus of the encode's)."""
     device = torch.device("cuda", _device_index(device))   # 'cuda' = the current device, resolved once
-    key = (device.index, reserve_cus, confine_decode and reserve_cus > 0, lanes)
+    ndec = (reserve_cus if confine_decode is True else int(confine_decode or 0)) if reserve_cus > 0 else 0
+    key = (device.index, reserve_cus, ndec, lanes)
     if key in _STREAM_SETS:
         return _STREAM_SETS[key][:2]
     lo, hi = torch.cuda.Stream.priority_range()
@@ -71,12 +74,12 @@ def _stream_set(device, reserve_cus: int, confine_decode: bool, lanes: int):
             s_enc = torch.cuda.ExternalStream(h.value, device=device)
         else:
             s_enc = torch.cuda.Stream(device, priority=lo)
-        if confine_decode and reserve_cus > 0:
-            # decode streams masked to exactly the reserved CUs: decode workgroups never take an
-            # encode CU between two GEMM workgroups
+        if ndec > 0:
+            # decode streams masked to the reserved CUs (plus, for ndec > reserve_cus, some of the
+            # encode's): decode workgroups never take the other encode CUs between two GEMM workgroups
             words = (torch.cuda.get_device_properties(device).multi_processor_count + 31) // 32
             mask = (C.c_uint32 * words)()
-            for c in range(reserve_cus):
+            for c in range(ndec):
                 mask[c // 32] |= 1 << (c % 32)
             s_decs = []
             for _ in range(lanes):
@@ -118,7 +121,7 @@ atexit.register(_release_at_exit)
 class CaptionPipeline:
     def __init__(self, encoder: HipViTEncoder, prefix: HipPrefix, decoder: HipGPT2Decoder, cfg: GenConfig,
                  batch: int, prompt_ids: Sequence[int], device, depth: int = 2, gather=None,
-                 reserve_cus: int = 0, dec_lanes: int = 1, confine_decode: bool = False, dec_group: int = 1,
+                 reserve_cus: int = 0, dec_lanes: int = 1, confine_decode: Union[bool, int] = False, dec_group: int = 1,
                  enc_group: int = 1):
         self.enc, self.pre, self.dec, self.cfg = encoder, prefix, decoder, cfg
         self.prompt_ids = list(prompt_ids)
@@ -139,7 +142,9 @@ class CaptionPipeline:
         # The decode chain is latency-bound: give its stream the higher priority so its small
         # workgroups are dispatched as soon as encode GEMM workgroups retire, and optionally keep
         # the encode off `reserve_cus` CUs (a CU-masked stream) so the decode always finds some.
-        self.s_enc, self.s_decs = _stream_set(self.device, int(reserve_cus), bool(confine_decode), self.lanes)
+        self.s_enc, self.s_decs = _stream_set(self.device, int(reserve_cus),
+                                              confine_decode if isinstance(confine_decode, bool) else int(confine_decode),
+                                              self.lanes)
         self.s_dec = self.s_decs[0]
         # the encoder / decoder workspaces are shared with serial calls made on the creating stream:
         # nothing of the pipeline may start before that stream's pending work has finished

@@ -59,7 +59,7 @@ def _stream_set(device, reserve_cus: int, confine_decode, lanes: int):
     """confine_decode: False = decode lanes unmasked; True = masked to the reserved CUs; an int n > 1 =
     masked to the first n CUs (the reserved ones plus n - reserve_cus of the encode's)."""
     device = torch.device("cuda", _device_index(device))   # 'cuda' = the current device, resolved once
-    ndec = (reserve_cus if confine_decode is True else int(confine_decode or 0)) if reserve_cus > 0 else 0
+    ndec = reserve_cus if confine_decode is True else int(confine_decode or 0)
     key = (device.index, reserve_cus, ndec, lanes)
     if key in _STREAM_SETS:
         return _STREAM_SETS[key][:2]
